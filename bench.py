@@ -1,0 +1,179 @@
+"""bench.py — L7 verdicts/s (+ HBM roofline fraction) on BASELINE.json's
+headline workload: config 2, 1k HTTP path/method/host/header regex rules,
+64M synthetic requests per GPU, inputs resident in HBM.
+
+One step = one l7m_eval_device pass over the rank's whole batch (+ the RCCL
+all-reduce of the per-rule hit/deny counters when N > 1).  Requests are
+sharded across ranks (each rank generates its own contiguous shard of the
+same deterministic workload), so scaling is weak.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--requests R]
+N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from cilium_amd import l7match as L  # noqa: E402
+from cilium_amd import workloads as W  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--requests", type=int, default=0, help="requests per GPU (default: config's)")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, rules, seconds, threads):
+    """Oracle (the reference algorithm restated: per-request linear rule scan,
+    std::regex_match per matcher) timed on the host on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import HttpOracle, KafkaOracle  # test infrastructure: cpu_baseline leg only
+    proto = W.CONFIGS[cfg]["proto"]
+    orc = HttpOracle(rules) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+    # calibrate on a small sample, then size the timed sample to ~`seconds`
+    a, o = W.requests(cfg, 10_000_000, 20_000, threads=threads)
+    t = time.perf_counter()
+    orc.eval(a, o, threads=threads)
+    rate = 20_000 / max(1e-6, time.perf_counter() - t)
+    n = int(min(20_000_000, max(20_000, rate * seconds)))
+    a, o = W.requests(cfg, 20_000_000, n, threads=threads)
+    t = time.perf_counter()
+    orc.eval(a, o, threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": n / dt, "unit": "verdicts/s", "cores": threads, "kind": "port",
+            "sample": f"{n} requests of config {cfg} (requests [20M, 20M+{n})), {dt:.1f} s, "
+                      f"oracle/l7oracle.cc (std::regex_match linear rule scan) on {threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = args.config
+    c = W.CONFIGS[cfg]
+    per_gpu = args.requests or c["n_requests"]
+    threads = args.threads or max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+
+    rules = W.rules(cfg)
+    rs = L.RuleSet.compile_http(rules) if c["proto"] == L.PROTO_HTTP else L.RuleSet.compile_kafka(rules)
+
+    # ---- rank's shard, generated deterministically, resident in HBM --------
+    t0 = time.perf_counter()
+    arena, offs = W.requests(cfg, rank * per_gpu, per_gpu, threads=threads)
+    gen_s = time.perf_counter() - t0
+    rec_bytes = int(offs[-1]) + int(np.frombuffer(arena[int(offs[-1]):int(offs[-1]) + 4].tobytes(), np.uint32)[0])
+    rec_bytes = (rec_bytes + 3) & ~3
+    pinned = torch.from_numpy(arena).pin_memory()
+    d_arena = torch.empty(arena.nbytes, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d_arena.copy_(pinned, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_s = time.perf_counter() - t0
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+    arena_nbytes = arena.nbytes
+    del pinned, arena, offs
+    d_verd = torch.empty(per_gpu, dtype=torch.int32, device=dev)
+    d_hits = torch.zeros(rs.n_counters, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        d_hits.zero_()
+        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, d_hits, stream.cuda_stream)
+        if world > 1:
+            dist.all_reduce(d_hits)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    for i in range(args.steps):
+        d_hits.zero_()
+        ev[i][0].record(stream)
+        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, d_hits, stream.cuda_stream)
+        ev[i][1].record(stream)
+        if world > 1:
+            dist.all_reduce(d_hits)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    total_requests = per_gpu * world * args.steps
+    value = total_requests / elapsed
+    kavg = float(np.mean(kernel_ms)) / 1e3
+    # algorithmic bytes per launch: records + u64 offset + i32 verdict per request (+ counters)
+    alg_bytes = rec_bytes + 12 * per_gpu + 8 * rs.n_counters
+    achieved = alg_bytes / kavg / 1e9
+    # sanity: verdicts were produced for every request of every step
+    hits_total = int(d_hits.sum().item())
+    expect_hits = per_gpu * world
+
+    if rank == 0:
+        res = {
+            "metric": "L7 verdicts/sec (HTTP reqs, 1k rules) + achieved HBM GB/s vs peak",
+            "value": value,
+            "unit": "verdicts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (deterministic generator libl7gen.so, SURVEY.md §8(d))",
+            "config": {"workload": c["name"], "baseline_config": cfg, "n_rules": len(rules),
+                       "requests_per_gpu": per_gpu, "seed": hex(c["seed"]),
+                       "mean_record_bytes": rec_bytes / per_gpu,
+                       "parallelism": f"dp{world} (request-sharded, RCCL all-reduce of {rs.n_counters} counters)",
+                       "dfa_groups": int(rs.info.n_dfas), "dfa_states": int(rs.info.total_dfa_states)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_launch": alg_bytes},
+            "counters_ok": hits_total == expect_hits,
+            "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds, threads)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,487 @@
+// http_compile.cc — compile []PortRuleHTTP into the HTTP device program.
+//
+// Pipeline (cold path, once per policy revision):
+//   1. getHTTPRule (pkg/envoy/server.go:261-320): PortRuleHTTP -> HeaderMatcher
+//      list, sorted by SortHeaderMatchers (pkg/envoy/sort.go:205-250).  Equal
+//      (Name, Value) pairs involving a header matcher make Go dereference a nil
+//      Regex and panic (sort.go:225-228); we return L7M_EINVAL_RULE instead.
+//   2. Envoy HeaderData (envoy/cilium_network_policy.h:52-66 -> upstream
+//      ConfigUtility::HeaderData): name lower-cased; empty value -> Present,
+//      regex flag -> Regex (std::regex(value, optimize): throws -> NACK, here
+//      L7M_EINVAL_REGEX), else exact Value.
+//   3. Fields: ":method", ":path", ":authority", then every other header name
+//      a rule references.  Per field, the distinct Regex/Value patterns are
+//      determinised together into DFA groups (split when a group exceeds the
+//      state/table limits); a header-name DFA maps request header names to
+//      field ids.
+//   4. First-match index: every rule is "keyed" on its most selective matcher.
+//      For each (DFA, end set) the sorted list of rules keyed on a pattern of
+//      that set is precomputed; at run time the kernel scans those lists in
+//      rule order and verifies the rule's remaining matchers (AND), giving the
+//      smallest matching rule index = HttpNetworkPolicyRule OR semantics
+//      (envoy/cilium_network_policy.h:98-105) with a deterministic index.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <regex>
+#include <unordered_map>
+
+#include "l7m_internal.h"
+#include "program.h"
+#include "regex_ecma.h"
+
+namespace l7m {
+namespace {
+
+std::string cstr(const char* p) { return p ? std::string(p) : std::string(); }
+
+// Go strings.SplitN(s, " ", 2)
+std::vector<std::string> split2(const std::string& s) {
+  size_t k = s.find(' ');
+  if (k == std::string::npos) return {s};
+  return {s.substr(0, k), s.substr(k + 1)};
+}
+
+// Go strings.TrimRight(s, ":")
+std::string trim_right_colon(std::string s) {
+  while (!s.empty() && s.back() == ':') s.pop_back();
+  return s;
+}
+
+// HeaderMatcherLess (pkg/envoy/sort.go:209-233) without the nil dereference;
+// the caller rejects the inputs where Go would panic.
+bool matcher_less(const HeaderMatcher& a, const HeaderMatcher& b) {
+  if (a.name != b.name) return a.name < b.name;
+  if (a.value != b.value) return a.value < b.value;
+  bool ar = a.has_regex && a.regex, br = b.has_regex && b.regex;
+  return !ar && br;
+}
+
+struct FieldPattern {
+  MatchKind kind;
+  std::string value;
+  bool operator<(const FieldPattern& o) const {
+    if (kind != o.kind) return kind < o.kind;
+    return value < o.value;
+  }
+};
+
+struct Group {
+  std::vector<uint32_t> pats;  // field pattern indices (local id = position)
+  re::Dfa dfa;
+};
+
+int build_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> idx,
+                 const re::DfaLimits& lim, std::vector<Group>* out, std::string* err) {
+  std::vector<const re::Ast*> sub;
+  for (uint32_t i : idx) sub.push_back(asts[i]);
+  Group g;
+  re::Status st = re::build_dfa(sub, lim, &g.dfa);
+  if (st == re::Status::Ok) {
+    g.pats = std::move(idx);
+    out->push_back(std::move(g));
+    return L7M_OK;
+  }
+  if (st != re::Status::TooBig) {
+    *err = "DFA construction failed";
+    return L7M_EUNSUPPORTED;
+  }
+  if (idx.size() == 1) {
+    *err = "a single pattern exceeds the DFA state/table limit";
+    return L7M_ETOOBIG;
+  }
+  size_t h = idx.size() / 2;
+  std::vector<uint32_t> a(idx.begin(), idx.begin() + h), b(idx.begin() + h, idx.end());
+  int rc = build_groups(asts, std::move(a), lim, out, err);
+  if (rc != L7M_OK) return rc;
+  return build_groups(asts, std::move(b), lim, out, err);
+}
+
+}  // namespace
+
+std::string lower_ascii(const std::string& s) {
+  std::string r = s;
+  for (auto& c : r)
+    if (c >= 'A' && c <= 'Z') c = static_cast<char>(c - 'A' + 'a');
+  return r;
+}
+
+MatchKind envoy_kind(const HeaderMatcher& m) {
+  if (m.value.empty()) return MatchKind::Present;
+  if (m.has_regex && m.regex) return MatchKind::Regex;
+  return MatchKind::Value;
+}
+
+int translate_http_rule(const l7m_http_rule& r, std::vector<HeaderMatcher>* out, std::string* err) {
+  out->clear();
+  std::string path = cstr(r.path), method = cstr(r.method), host = cstr(r.host);
+  if (!path.empty()) out->push_back({":path", path, true, true});
+  if (!method.empty()) out->push_back({":method", method, true, true});
+  if (!host.empty()) out->push_back({":authority", host, true, true});
+  for (uint32_t j = 0; j < r.n_headers; ++j) {
+    if (!r.headers) {
+      *err = "headers == NULL with n_headers > 0";
+      return L7M_EINVAL;
+    }
+    auto parts = split2(cstr(r.headers[j]));
+    if (parts.size() == 2) out->push_back({trim_right_colon(parts[0]), parts[1], false, false});
+    else out->push_back({parts[0], "", false, false});
+  }
+  // SortHeaderMatchers panics on equal (Name, Value) with a nil Regex.
+  for (size_t a = 0; a < out->size(); ++a)
+    for (size_t b = a + 1; b < out->size(); ++b) {
+      const auto& x = (*out)[a];
+      const auto& y = (*out)[b];
+      if (x.name == y.name && x.value == y.value && !(x.has_regex && y.has_regex)) {
+        *err = "duplicate header matcher '" + x.name + "' (getHTTPRule sort would panic, "
+               "pkg/envoy/sort.go:225-228)";
+        return L7M_EINVAL_RULE;
+      }
+    }
+  std::stable_sort(out->begin(), out->end(), matcher_less);
+  for (const auto& m : *out)
+    if (m.name.empty()) {
+      // Envoy's HeaderMatcher.name validation (min_bytes 1) rejects the policy.
+      *err = "empty header name";
+      return L7M_EINVAL_RULE;
+    }
+  return L7M_OK;
+}
+
+CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts& opts) {
+  CompileResult res;
+  auto fail = [&](int st, const std::string& m) {
+    res.status = st;
+    res.err = m;
+    return res;
+  };
+  if (n > 0 && !rules) return fail(L7M_EINVAL, "rules == NULL");
+  if (opts.dialect != L7M_DIALECT_ENVOY_ECMA_FULL)
+    return fail(L7M_EUNSUPPORTED, "only L7M_DIALECT_ENVOY_ECMA_FULL is implemented");
+  if (n >= kNone / 2) return fail(L7M_ETOOBIG, "too many rules");
+
+  // 1-2. translate, field/pattern assignment
+  std::vector<std::string> field_names = {":method", ":path", ":authority"};
+  std::unordered_map<std::string, uint32_t> field_of = {
+      {":method", kFieldMethod}, {":path", kFieldPath}, {":authority", kFieldAuthority}};
+  std::vector<std::map<FieldPattern, uint32_t>> fpat_idx(3);
+  std::vector<std::vector<FieldPattern>> fpats(3);
+
+  struct RM {
+    uint32_t field;
+    MatchKind kind;
+    uint32_t fpat;  // field pattern index (kNone for Present)
+  };
+  std::vector<std::vector<RM>> rule_m(n);
+  std::vector<HeaderMatcher> hm;
+  for (size_t i = 0; i < n; ++i) {
+    std::string err;
+    int rc = translate_http_rule(rules[i], &hm, &err);
+    if (rc != L7M_OK) return fail(rc, "rule " + std::to_string(i) + ": " + err);
+    for (const auto& m : hm) {
+      std::string lname = lower_ascii(m.name);  // Envoy LowerCaseString
+      auto it = field_of.find(lname);
+      uint32_t f;
+      if (it == field_of.end()) {
+        f = static_cast<uint32_t>(field_names.size());
+        if (f >= kMaxFields)
+          return fail(L7M_ETOOBIG, "more than 64 distinct header fields referenced");
+        field_of.emplace(lname, f);
+        field_names.push_back(lname);
+        fpat_idx.emplace_back();
+        fpats.emplace_back();
+      } else {
+        f = it->second;
+      }
+      MatchKind k = envoy_kind(m);
+      RM r{f, k, kNone};
+      if (k != MatchKind::Present) {
+        FieldPattern fp{k, m.value};
+        auto pit = fpat_idx[f].find(fp);
+        if (pit == fpat_idx[f].end()) {
+          pit = fpat_idx[f].emplace(fp, static_cast<uint32_t>(fpats[f].size())).first;
+          fpats[f].push_back(fp);
+        }
+        r.fpat = pit->second;
+      }
+      rule_m[i].push_back(r);
+    }
+  }
+  const uint32_t nf = static_cast<uint32_t>(field_names.size());
+
+  // 3. parse patterns and build DFA groups per field
+  re::DfaLimits lim;
+  if (opts.max_dfa_states) lim.max_states = opts.max_dfa_states;
+  if (opts.max_table_bytes) lim.max_table_bytes = opts.max_table_bytes;
+  std::vector<std::vector<Group>> groups(nf);
+  // field pattern -> (group, local id)
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fp_loc(nf);
+  for (uint32_t f = 0; f < nf; ++f) {
+    if (fpats[f].empty()) continue;
+    std::vector<re::Ast> asts(fpats[f].size());
+    std::vector<const re::Ast*> ptrs;
+    for (size_t p = 0; p < fpats[f].size(); ++p) {
+      const auto& fp = fpats[f][p];
+      if (fp.kind == MatchKind::Regex) {
+        try {
+          std::regex probe(fp.value, std::regex::ECMAScript | std::regex::optimize);
+          (void)probe;
+        } catch (const std::regex_error& e) {
+          return fail(L7M_EINVAL_REGEX, "invalid regex '" + fp.value + "' on " + field_names[f] +
+                                            ": " + e.what() + " (Envoy would NACK the policy)");
+        }
+        std::string perr;
+        re::Status st = re::parse_ecma(fp.value, &asts[p], &perr);
+        if (st == re::Status::TooBig)
+          return fail(L7M_ETOOBIG, "regex '" + fp.value + "': " + perr);
+        if (st != re::Status::Ok)
+          return fail(L7M_EUNSUPPORTED, "regex '" + fp.value + "': " + perr +
+                                            " is outside the compiled (regular) subset");
+      } else {
+        asts[p] = re::literal_ast(fp.value);
+      }
+      ptrs.push_back(&asts[p]);
+    }
+    std::vector<uint32_t> idx(fpats[f].size());
+    for (uint32_t p = 0; p < idx.size(); ++p) idx[p] = p;
+    std::string err;
+    int rc = build_groups(ptrs, idx, lim, &groups[f], &err);
+    if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+    fp_loc[f].assign(fpats[f].size(), {0, 0});
+    for (uint32_t g = 0; g < groups[f].size(); ++g)
+      for (uint32_t l = 0; l < groups[f][g].pats.size(); ++l)
+        fp_loc[f][groups[f][g].pats[l]] = {g, l};
+  }
+
+  // header-name DFA over every regular field name (exact, lower-case)
+  bool has_name = nf > 3;
+  re::Dfa name_dfa;
+  if (has_name) {
+    std::vector<re::Ast> asts;
+    for (uint32_t f = 3; f < nf; ++f) asts.push_back(re::literal_ast(field_names[f]));
+    std::vector<const re::Ast*> ptrs;
+    for (auto& a : asts) ptrs.push_back(&a);
+    re::DfaLimits nl;
+    nl.max_states = 1u << 22;
+    nl.max_table_bytes = 1ull << 30;
+    if (re::build_dfa(ptrs, nl, &name_dfa) != re::Status::Ok)
+      return fail(L7M_ETOOBIG, "header-name DFA too large");
+  }
+
+  // global DFA numbering: fields in order, groups in order
+  std::vector<uint32_t> dfa_first(nf, 0);
+  uint32_t ndfa = 0;
+  for (uint32_t f = 0; f < nf; ++f) {
+    dfa_first[f] = ndfa;
+    ndfa += static_cast<uint32_t>(groups[f].size());
+  }
+
+  // 4. keys: most selective matcher per rule
+  std::vector<std::vector<uint32_t>> share(nf);
+  for (uint32_t f = 0; f < nf; ++f) share[f].assign(fpats[f].size(), 0);
+  for (size_t i = 0; i < n; ++i) {
+    std::vector<std::pair<uint32_t, uint32_t>> seen;
+    for (const auto& m : rule_m[i])
+      if (m.fpat != kNone) {
+        auto key = std::make_pair(m.field, m.fpat);
+        if (std::find(seen.begin(), seen.end(), key) == seen.end()) {
+          seen.push_back(key);
+          share[m.field][m.fpat]++;
+        }
+      }
+  }
+  auto field_rank = [](uint32_t f) -> uint32_t {
+    if (f == kFieldPath) return 0;
+    if (f == kFieldAuthority) return 1;
+    if (f == kFieldMethod) return 3;
+    return 2;
+  };
+  // keyed lists
+  std::vector<std::vector<std::vector<uint32_t>>> keyed(ndfa);  // [dfa][local pattern]
+  for (uint32_t f = 0; f < nf; ++f)
+    for (uint32_t g = 0; g < groups[f].size(); ++g)
+      keyed[dfa_first[f] + g].resize(groups[f][g].pats.size());
+  std::vector<std::vector<uint32_t>> pres_keyed(nf);
+  uint32_t always_rule = kNone;
+  std::vector<uint32_t> zero_list;  // no matchers, remote-restricted
+  std::vector<std::vector<uint32_t>> remotes(n);
+  bool any_remotes = true;
+  for (size_t i = 0; i < n; ++i) {
+    if (rules[i].n_remote_ids) {
+      if (!rules[i].remote_ids) return fail(L7M_EINVAL, "remote_ids == NULL with n_remote_ids > 0");
+      remotes[i].assign(rules[i].remote_ids, rules[i].remote_ids + rules[i].n_remote_ids);
+      std::sort(remotes[i].begin(), remotes[i].end());
+      remotes[i].erase(std::unique(remotes[i].begin(), remotes[i].end()), remotes[i].end());
+      any_remotes = false;
+    }
+  }
+  for (size_t i = 0; i < n; ++i) {
+    if (rule_m[i].empty()) {
+      if (!remotes[i].empty()) zero_list.push_back(static_cast<uint32_t>(i));
+      else if (always_rule == kNone) always_rule = static_cast<uint32_t>(i);
+      continue;
+    }
+    const RM* best = nullptr;
+    auto score = [&](const RM& m) {
+      uint64_t pres = m.kind == MatchKind::Present ? 1 : 0;
+      uint64_t sh = m.fpat == kNone ? 0xffffffffu : share[m.field][m.fpat];
+      return (pres << 60) | (sh << 8) | field_rank(m.field);
+    };
+    for (const auto& m : rule_m[i])
+      if (!best || score(m) < score(*best)) best = &m;
+    if (best->kind == MatchKind::Present) {
+      pres_keyed[best->field].push_back(static_cast<uint32_t>(i));
+    } else {
+      auto loc = fp_loc[best->field][best->fpat];
+      keyed[dfa_first[best->field] + loc.first][loc.second].push_back(static_cast<uint32_t>(i));
+    }
+  }
+
+  // ---- assemble the program -------------------------------------------
+  std::vector<uint32_t> pool;
+  auto push_list = [&](const std::vector<uint32_t>& v) -> Span {
+    Span s{static_cast<uint32_t>(pool.size()), static_cast<uint32_t>(v.size())};
+    pool.insert(pool.end(), v.begin(), v.end());
+    return s;
+  };
+
+  struct DfaOut {
+    const re::Dfa* d;
+    uint32_t field;
+  };
+  std::vector<DfaOut> all;
+  for (uint32_t f = 0; f < nf; ++f)
+    for (auto& g : groups[f]) all.push_back({&g.dfa, f});
+  if (has_name) all.push_back({&name_dfa, kNone});
+  const uint32_t ndt = static_cast<uint32_t>(all.size());
+
+  std::vector<DfaDesc> dd(ndt);
+  std::vector<Span> sets, cands;
+  uint64_t table_words = 0, total_states = 0;
+  for (uint32_t k = 0; k < ndt; ++k) {
+    const re::Dfa& d = *all[k].d;
+    dd[k].ncols = static_cast<uint32_t>(d.ncls) + 1;
+    dd[k].start = static_cast<uint32_t>(d.start) * dd[k].ncols;
+    dd[k].set_base = static_cast<uint32_t>(sets.size());
+    dd[k].nsets = static_cast<uint32_t>(d.sets.size());
+    dd[k].field = all[k].field;
+    dd[k].nstates = static_cast<uint32_t>(d.nstates);
+    dd[k].cmap_index = k;
+    dd[k].table_off = static_cast<uint32_t>(table_words);  // relative for now
+    uint64_t words = static_cast<uint64_t>(d.nstates) * dd[k].ncols;
+    if (words >= (1ull << 32)) return fail(L7M_ETOOBIG, "DFA table offset overflow");
+    table_words += words;
+    total_states += d.nstates;
+    for (size_t s = 0; s < d.sets.size(); ++s) {
+      sets.push_back(push_list(d.sets[s]));
+      if (k < ndfa) {
+        std::vector<uint32_t> c;
+        for (uint32_t p : d.sets[s]) {
+          const auto& kl = keyed[k][p];
+          c.insert(c.end(), kl.begin(), kl.end());
+        }
+        std::sort(c.begin(), c.end());
+        c.erase(std::unique(c.begin(), c.end()), c.end());
+        cands.push_back(push_list(c));
+      } else {
+        cands.push_back(Span{0, 0});
+      }
+    }
+  }
+  std::vector<uint32_t> name_field;
+  if (has_name) {
+    for (const auto& s : name_dfa.sets) name_field.push_back(s.empty() ? kNone : 3 + s[0]);
+  }
+  std::vector<FieldDesc> fd(nf);
+  for (uint32_t f = 0; f < nf; ++f) {
+    fd[f].dfa_first = dfa_first[f];
+    fd[f].ndfa = static_cast<uint32_t>(groups[f].size());
+    fd[f].presence = push_list(pres_keyed[f]);
+  }
+  std::vector<Span> rspan(n), rremote(n);
+  for (size_t i = 0; i < n; ++i) rremote[i] = push_list(remotes[i]);
+  Span zero_span = push_list(zero_list);
+  std::vector<MatcherDesc> md;
+  for (size_t i = 0; i < n; ++i) {
+    rspan[i] = Span{static_cast<uint32_t>(md.size()), static_cast<uint32_t>(rule_m[i].size())};
+    for (const auto& m : rule_m[i]) {
+      MatcherDesc x{m.field, m.kind == MatchKind::Present ? 1u : 0u, kNone, kNone};
+      if (m.fpat != kNone) {
+        auto loc = fp_loc[m.field][m.fpat];
+        x.dfa = dfa_first[m.field] + loc.first;
+        x.pattern = loc.second;
+      }
+      md.push_back(x);
+    }
+  }
+
+  // layout
+  HttpHeader h;
+  std::memset(&h, 0, sizeof h);
+  uint64_t w = sizeof(HttpHeader) / 4;
+  auto take = [&](uint64_t words) {
+    uint64_t o = w;
+    w += words;
+    return static_cast<uint32_t>(o);
+  };
+  h.magic = kMagicHttp;
+  h.n_rules = static_cast<uint32_t>(n);
+  h.n_fields = nf;
+  h.n_dfas = ndfa;
+  h.always_rule = always_rule;
+  h.allow_no_l7 = n == 0 ? 1u : 0u;
+  h.has_name_dfa = has_name ? 1u : 0u;
+  h.off_dfas = take(static_cast<uint64_t>(ndt) * sizeof(DfaDesc) / 4);
+  h.off_fields = take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
+  h.off_name_field = take(name_field.size());
+  h.off_sets = take(sets.size() * 2);
+  h.off_cands = take(cands.size() * 2);
+  h.off_rules = take(static_cast<uint64_t>(n) * 2);
+  h.off_matchers = take(md.size() * 4);
+  h.off_remotes = take(static_cast<uint64_t>(n) * 2);
+  h.any_remotes = any_remotes ? 1u : 0u;
+  h.zero_list = zero_span;
+  h.off_pool = take(pool.size());
+  w = (w + 63) & ~uint64_t(63);  // 256-byte align tables
+  h.off_tables = take(table_words);
+  h.table_words = static_cast<uint32_t>(table_words);
+  h.off_cmaps = take(static_cast<uint64_t>(ndt) * 64);
+  if (w >= (1ull << 32)) return fail(L7M_ETOOBIG, "program exceeds 16 GiB");
+  h.total_words = static_cast<uint32_t>(w);
+
+  std::vector<uint32_t> prog(w, 0);
+  std::memcpy(prog.data(), &h, sizeof h);
+  for (uint32_t k = 0; k < ndt; ++k) {
+    dd[k].table_off += h.off_tables;
+    const re::Dfa& d = *all[k].d;
+    uint32_t nc = dd[k].ncols;
+    uint32_t* t = prog.data() + dd[k].table_off;
+    for (int s = 0; s < d.nstates; ++s) {
+      for (int c = 0; c < d.ncls; ++c) t[static_cast<size_t>(s) * nc + c] = d.next[static_cast<size_t>(s) * d.ncls + c] * nc;
+      t[static_cast<size_t>(s) * nc + d.ncls] = d.endset[s];
+    }
+    std::memcpy(reinterpret_cast<uint8_t*>(prog.data() + h.off_cmaps) + 256 * k, d.cmap, 256);
+  }
+  std::memcpy(prog.data() + h.off_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
+  std::memcpy(prog.data() + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));
+  if (!name_field.empty())
+    std::memcpy(prog.data() + h.off_name_field, name_field.data(), name_field.size() * 4);
+  std::memcpy(prog.data() + h.off_sets, sets.data(), sets.size() * sizeof(Span));
+  std::memcpy(prog.data() + h.off_cands, cands.data(), cands.size() * sizeof(Span));
+  if (n) std::memcpy(prog.data() + h.off_rules, rspan.data(), rspan.size() * sizeof(Span));
+  if (n) std::memcpy(prog.data() + h.off_remotes, rremote.data(), rremote.size() * sizeof(Span));
+  if (!md.empty()) std::memcpy(prog.data() + h.off_matchers, md.data(), md.size() * sizeof(MatcherDesc));
+  if (!pool.empty()) std::memcpy(prog.data() + h.off_pool, pool.data(), pool.size() * 4);
+
+  res.program = std::move(prog);
+  res.info.proto = L7M_PROTO_HTTP;
+  res.info.n_rules = static_cast<uint32_t>(n);
+  res.info.n_fields = nf;
+  res.info.n_dfas = ndt;
+  res.info.total_dfa_states = total_states;
+  res.info.program_bytes = static_cast<uint64_t>(w) * 4;
+  res.info.n_counters = static_cast<uint32_t>(n) + 2;
+  return res;
+}
+
+}  // namespace l7m

@@ -1,0 +1,321 @@
+// l7m_api.cc — the C ABI of libl7match.so (include/l7match.h).
+//
+// Compilation runs on the host (cold path); evaluation always runs on the GPU.
+// There is no CPU evaluation path in this library: without a HIP device the
+// eval entry points return L7M_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/l7match.h"
+#include "l7m_device.h"
+#include "l7m_internal.h"
+#include "program.h"
+
+using namespace l7m;
+
+namespace {
+
+void set_err(char* err, size_t errlen, const std::string& m) {
+  if (!err || errlen == 0) return;
+  size_t k = m.size() < errlen - 1 ? m.size() : errlen - 1;
+  std::memcpy(err, m.data(), k);
+  err[k] = '\0';
+}
+
+l7m_opts norm_opts(const l7m_opts* o) {
+  l7m_opts r{};
+  if (o && o->struct_size >= sizeof(l7m_opts)) r = *o;
+  else if (o && o->struct_size == 0) r = *o;
+  return r;
+}
+
+int finish_compile(CompileResult&& cr, uint32_t proto, l7m_ruleset** out, char* err, size_t errlen) {
+  if (cr.status != L7M_OK) {
+    set_err(err, errlen, cr.err);
+    return cr.status;
+  }
+  auto* rs = new (std::nothrow) l7m_ruleset();
+  if (!rs) return L7M_ENOMEM;
+  rs->proto = proto;
+  rs->program = std::move(cr.program);
+  rs->info = cr.info;
+  *out = rs;
+  return L7M_OK;
+}
+
+int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return L7M_EDEVICE;
+  if (dev < 0 || dev >= 64) return L7M_EDEVICE;
+  hipDeviceProp_t prop;
+  static thread_local int cached_dev = -1, cached_cus = 0;
+  if (cached_dev != dev) {
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return L7M_EDEVICE;
+    cached_dev = dev;
+    cached_cus = prop.multiProcessorCount;
+  }
+  *cus = cached_cus;
+  std::lock_guard<std::mutex> g(rs->mu);
+  if (!rs->dprog[dev]) {
+    void* p = nullptr;
+    size_t bytes = rs->program.size() * 4;
+    if (hipMalloc(&p, bytes) != hipSuccess) return L7M_ENOMEM;
+    if (hipMemcpy(p, rs->program.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      hipFree(p);
+      return L7M_EDEVICE;
+    }
+    rs->dprog[dev] = p;
+  }
+  *out = static_cast<const uint32_t*>(rs->dprog[dev]);
+  return L7M_OK;
+}
+
+int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const void* offs, size_t n, void* verdicts,
+           void* hits, hipStream_t stream) {
+  auto* rs = const_cast<l7m_ruleset*>(crs);
+  const uint32_t* dprog = nullptr;
+  int cus = 0;
+  int rc = device_program(rs, &dprog, &cus);
+  if (rc != L7M_OK) return rc;
+  hipError_t e;
+  if (rs->proto == L7M_PROTO_HTTP) {
+    HttpHeader h;
+    std::memcpy(&h, rs->program.data(), sizeof h);
+    if (http_lds_bytes(h, 256) > 160 * 1024) return L7M_ETOOBIG;
+    e = launch_http(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
+                    n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
+                    stream, cus);
+  } else if (rs->proto == L7M_PROTO_KAFKA) {
+    KafkaHeader h;
+    std::memcpy(&h, rs->program.data(), sizeof h);
+    e = launch_kafka(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
+                     n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
+                     stream, cus);
+  } else {
+    return L7M_EINVAL;
+  }
+  return e == hipSuccess ? L7M_OK : L7M_EDEVICE;
+}
+
+}  // namespace
+
+extern "C" {
+
+int l7m_abi_version(void) { return L7M_ABI_VERSION; }
+
+int l7m_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int l7m_compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts* opts, l7m_ruleset** out,
+                     char* err, size_t errlen) {
+  if (!out) return L7M_EINVAL;
+  try {
+    return finish_compile(compile_http(rules, n, norm_opts(opts)), L7M_PROTO_HTTP, out, err, errlen);
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of host memory");
+    return L7M_ENOMEM;
+  }
+}
+
+int l7m_compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts* opts,
+                      l7m_ruleset** out, char* err, size_t errlen) {
+  if (!out) return L7M_EINVAL;
+  try {
+    return finish_compile(compile_kafka(rules, n, norm_opts(opts)), L7M_PROTO_KAFKA, out, err, errlen);
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of host memory");
+    return L7M_ENOMEM;
+  }
+}
+
+void l7m_retain(l7m_ruleset* rs) {
+  if (rs) rs->refs.fetch_add(1);
+}
+
+void l7m_release(l7m_ruleset* rs) {
+  if (!rs) return;
+  if (rs->refs.fetch_sub(1) != 1) return;
+  for (int d = 0; d < 64; ++d)
+    if (rs->dprog[d]) {
+      int cur = 0;
+      hipGetDevice(&cur);
+      hipSetDevice(d);
+      hipFree(rs->dprog[d]);
+      hipSetDevice(cur);
+    }
+  delete rs;
+}
+
+int l7m_ruleset_get_info(const l7m_ruleset* rs, l7m_ruleset_info* out) {
+  if (!rs || !out) return L7M_EINVAL;
+  *out = rs->info;
+  return L7M_OK;
+}
+
+int l7m_ruleset_program(const l7m_ruleset* rs, void* buf, size_t* len) {
+  if (!rs || !len) return L7M_EINVAL;
+  size_t bytes = rs->program.size() * 4;
+  if (buf) {
+    if (*len < bytes) return L7M_EINVAL;
+    std::memcpy(buf, rs->program.data(), bytes);
+  }
+  *len = bytes;
+  return L7M_OK;
+}
+
+int l7m_http_translate(const l7m_http_rule* rule, l7m_header_matcher* out, size_t cap, char* err,
+                       size_t errlen) {
+  if (!rule) return L7M_EINVAL;
+  static thread_local std::vector<HeaderMatcher> hm;
+  std::string e;
+  int rc = translate_http_rule(*rule, &hm, &e);
+  if (rc != L7M_OK) {
+    set_err(err, errlen, e);
+    return rc;
+  }
+  for (size_t i = 0; i < hm.size() && i < cap && out; ++i) {
+    out[i].name = hm[i].name.c_str();
+    out[i].value = hm[i].value.c_str();
+    out[i].kind = static_cast<uint32_t>(envoy_kind(hm[i]));
+    out[i].has_regex_flag = hm[i].has_regex ? 1u : 0u;
+  }
+  return static_cast<int>(hm.size());
+}
+
+size_t l7m_http_record_size(const l7m_http_request* q) {
+  if (!q) return 0;
+  auto len = [](const char* s) -> size_t { return s ? std::strlen(s) : 0; };
+  size_t ml = len(q->method), pl = len(q->path), al = len(q->authority);
+  if (ml > 0xffff || pl > 0xffff || al > 0xffff || q->n_headers > 255) return 0;
+  size_t b = L7M_HTTP_REC_FIXED + 4u * q->n_headers + ml + pl + al;
+  for (uint32_t j = 0; j < q->n_headers; ++j) {
+    size_t nl = len(q->header_names[j]), vl = len(q->header_values[j]);
+    if (nl > 0xffff || vl > 0xffff) return 0;
+    b += nl + vl;
+  }
+  if (b > 0xffffffffu) return 0;
+  return (b + 3) & ~size_t(3);
+}
+
+size_t l7m_pack_http(const l7m_http_request* reqs, size_t n, uint8_t* arena, size_t cap,
+                     uint64_t* offsets) {
+  size_t used = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const l7m_http_request& q = reqs[i];
+    size_t sz = l7m_http_record_size(&q);
+    if (sz == 0 || used + sz > cap) return 0;
+    uint8_t* r = arena + used;
+    std::memset(r, 0, sz);
+    auto len = [](const char* s) -> uint32_t { return s ? static_cast<uint32_t>(std::strlen(s)) : 0; };
+    uint32_t ml = len(q.method), pl = len(q.path), al = len(q.authority);
+    uint32_t flags = (q.method ? L7M_HTTP_F_METHOD : 0) | (q.path ? L7M_HTTP_F_PATH : 0) |
+                     (q.authority ? L7M_HTTP_F_AUTHORITY : 0) | (q.ingress ? L7M_HTTP_F_INGRESS : 0);
+    uint32_t w[5];
+    size_t unpadded = L7M_HTTP_REC_FIXED + 4u * q.n_headers + ml + pl + al;
+    for (uint32_t j = 0; j < q.n_headers; ++j) unpadded += len(q.header_names[j]) + len(q.header_values[j]);
+    w[0] = static_cast<uint32_t>(unpadded);
+    w[1] = q.remote_id;
+    w[2] = q.dport | (flags << 16) | (q.n_headers << 24);
+    w[3] = ml | (pl << 16);
+    w[4] = al;
+    std::memcpy(r, w, sizeof w);
+    size_t p = L7M_HTTP_REC_FIXED;
+    for (uint32_t j = 0; j < q.n_headers; ++j) {
+      uint32_t e = len(q.header_names[j]) | (len(q.header_values[j]) << 16);
+      std::memcpy(r + p, &e, 4);
+      p += 4;
+    }
+    auto put = [&](const char* s, uint32_t l) {
+      if (l) std::memcpy(r + p, s, l);
+      p += l;
+    };
+    put(q.method, ml);
+    put(q.path, pl);
+    put(q.authority, al);
+    for (uint32_t j = 0; j < q.n_headers; ++j) {
+      uint32_t nl = len(q.header_names[j]);
+      for (uint32_t k = 0; k < nl; ++k) {
+        char c = q.header_names[j][k];
+        r[p + k] = static_cast<uint8_t>((c >= 'A' && c <= 'Z') ? c - 'A' + 'a' : c);
+      }
+      p += nl;
+      put(q.header_values[j], len(q.header_values[j]));
+    }
+    offsets[i] = used;
+    used += sz;
+  }
+  return used;
+}
+
+int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes,
+                    const void* d_offsets, size_t n, void* d_verdicts, void* d_hits,
+                    void* hip_stream, uint32_t flags) {
+  (void)flags;
+  if (!rs || (n && (!d_arena || !d_offsets || !d_verdicts))) return L7M_EINVAL;
+  return launch(rs, d_arena, arena_bytes, d_offsets, n, d_verdicts, d_hits, static_cast<hipStream_t>(hip_stream));
+}
+
+int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
+             const uint64_t* offsets, size_t n, int32_t* verdicts, uint64_t* hits, uint32_t flags) {
+  (void)flags;
+  if (!rs || (n && (!arena || !offsets || !verdicts))) return L7M_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return L7M_EDEVICE;
+  if (n == 0) return L7M_OK;
+  const size_t nctr = rs->info.n_counters;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return L7M_EDEVICE;
+  void *da = nullptr, *doff = nullptr, *dv = nullptr, *dh = nullptr;
+  int rc = L7M_OK;
+  auto cleanup = [&]() {
+    if (da) hipFree(da);
+    if (doff) hipFree(doff);
+    if (dv) hipFree(dv);
+    if (dh) hipFree(dh);
+    hipStreamDestroy(st);
+  };
+  // Pad the arena copy so that the kernels' aligned word loads never run past it.
+  size_t abytes = (arena_bytes + 64) & ~size_t(3);
+  if (hipMalloc(&da, abytes) != hipSuccess || hipMalloc(&doff, n * 8) != hipSuccess ||
+      hipMalloc(&dv, n * 4) != hipSuccess || (hits && hipMalloc(&dh, nctr * 8) != hipSuccess)) {
+    cleanup();
+    return L7M_ENOMEM;
+  }
+  bool ok = hipMemsetAsync(da, 0, abytes, st) == hipSuccess &&
+            hipMemcpyAsync(da, arena, arena_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(doff, offsets, n * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+            (!hits || hipMemsetAsync(dh, 0, nctr * 8, st) == hipSuccess);
+  if (!ok) rc = L7M_EDEVICE;
+  if (rc == L7M_OK) rc = launch(rs, da, arena_bytes, doff, n, dv, dh, st);
+  if (rc == L7M_OK &&
+      hipMemcpyAsync(verdicts, dv, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    rc = L7M_EDEVICE;
+  std::vector<uint64_t> hh;
+  if (rc == L7M_OK && hits) {
+    hh.resize(nctr);
+    if (hipMemcpyAsync(hh.data(), dh, nctr * 8, hipMemcpyDeviceToHost, st) != hipSuccess) rc = L7M_EDEVICE;
+  }
+  if (hipStreamSynchronize(st) != hipSuccess && rc == L7M_OK) rc = L7M_EDEVICE;
+  if (rc == L7M_OK && hits)
+    for (size_t i = 0; i < nctr; ++i) hits[i] += hh[i];
+  cleanup();
+  return rc;
+}
+
+int l7m_alloc_pinned(size_t bytes, void** out) {
+  if (!out) return L7M_EINVAL;
+  return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? L7M_OK : L7M_ENOMEM;
+}
+
+void l7m_free_pinned(void* p) {
+  if (p) hipHostFree(p);
+}
+
+}  // extern "C"

@@ -1,0 +1,21 @@
+// l7m_device.h — launch entry points of the HIP kernels (l7m_kernels.hip,
+// l7m_kafka.hip) used by the C ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "program.h"
+
+namespace l7m {
+
+size_t http_lds_bytes(const HttpHeader& h, uint32_t block);
+hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena,
+                       uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
+                       unsigned long long* hits, hipStream_t stream, int num_cus);
+
+hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena,
+                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
+                        unsigned long long* hits, hipStream_t stream, int num_cus);
+
+}  // namespace l7m

@@ -1,0 +1,49 @@
+// l7m_internal.h — host-side pieces shared by the compilers and the C ABI.
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/l7match.h"
+
+namespace l7m {
+
+// One getHTTPRule HeaderMatcher (pkg/envoy/server.go:261-320).
+struct HeaderMatcher {
+  std::string name;   // as emitted by getHTTPRule (not lower-cased)
+  std::string value;
+  bool has_regex = false;  // HeaderMatcher.Regex != nil
+  bool regex = false;      // Regex.Value
+};
+
+// Envoy HeaderData kind after construction (Regex / Value / Present).
+enum class MatchKind : uint32_t { Regex = 0, Value = 1, Present = 2 };
+
+struct CompileResult {
+  int status = L7M_OK;
+  std::string err;
+  std::vector<uint32_t> program;
+  l7m_ruleset_info info{};
+};
+
+int translate_http_rule(const l7m_http_rule& r, std::vector<HeaderMatcher>* out, std::string* err);
+MatchKind envoy_kind(const HeaderMatcher& m);
+std::string lower_ascii(const std::string& s);
+
+CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts& opts);
+CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts& opts);
+
+}  // namespace l7m
+
+// The opaque handle.  Immutable after compile except for the per-device
+// program copies, which are created lazily under `mu`.
+struct l7m_ruleset {
+  std::atomic<int> refs{1};
+  uint32_t proto = 0;
+  std::vector<uint32_t> program;
+  l7m_ruleset_info info{};
+  std::mutex mu;
+  void* dprog[64] = {nullptr};  // per HIP device
+};

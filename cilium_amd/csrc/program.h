@@ -1,0 +1,120 @@
+// program.h — layout of a compiled rule set as it lives in HBM.
+//
+// A compiled rule set is ONE flat array of uint32 words (the "program"),
+// uploaded once per device and read by the evaluation kernels through
+// scalar/vector loads.  All offsets are word offsets from the start of the
+// program.  The same struct definitions are used by the host compiler
+// (http_compile.cc / kafka_compile.cc) and the HIP kernels.
+#pragma once
+#include <stdint.h>
+
+namespace l7m {
+
+constexpr uint32_t kMagicHttp = 0x5048374cu;   // "L7HP"
+constexpr uint32_t kMagicKafka = 0x504b374cu;  // "L7KP"
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kMaxFields = 64;            // present-mask is one u64 per request
+
+// Field ids of the three pseudo headers Cilium's getHTTPRule emits
+// (pkg/envoy/server.go:276-289).  Regular header fields follow.
+constexpr uint32_t kFieldMethod = 0;
+constexpr uint32_t kFieldPath = 1;
+constexpr uint32_t kFieldAuthority = 2;
+
+struct Span {
+  uint32_t off, len;  // into the u32 pool
+};
+
+// One DFA group.  Table rows are (ncls + 1) words wide; entries hold the
+// *premultiplied* row offset of the next state (state * ncols), so a step is
+// one load:  s = tab[s + cmap[byte]].  Column ncls holds the end-set id
+// (patterns matched if the value ends in this state).  Row 0 is the dead
+// state (all entries 0, end set 0 = empty).
+struct DfaDesc {
+  uint32_t table_off;   // word offset of row 0
+  uint32_t ncols;       // ncls + 1
+  uint32_t start;       // premultiplied start row
+  uint32_t set_base;    // index of this DFA's set 0 in sets[] / cands[]
+  uint32_t nsets;
+  uint32_t field;       // field this DFA evaluates (kNone for the name DFA)
+  uint32_t nstates;
+  uint32_t cmap_index;  // 256-byte class map number
+};
+
+struct FieldDesc {
+  uint32_t dfa_first, ndfa;  // value DFAs of this field (contiguous)
+  Span presence;             // rules keyed on "field present" (sorted)
+};
+
+// Matcher of a rule: field must be present and, for kind 0, the value DFA
+// `dfa` must have matched local pattern `pattern`.
+struct MatcherDesc {
+  uint32_t field;
+  uint32_t kind;     // 0 = DFA pattern (regex or literal), 1 = presence
+  uint32_t dfa;
+  uint32_t pattern;
+};
+
+struct HttpHeader {
+  uint32_t magic;
+  uint32_t n_rules;
+  uint32_t n_fields;
+  uint32_t n_dfas;         // value DFAs; the name DFA (if any) is dfas[n_dfas]
+  uint32_t always_rule;    // smallest rule with zero matchers, or kNone
+  uint32_t allow_no_l7;    // rule list empty -> L7M_VERDICT_ALLOW_NO_L7
+  uint32_t has_name_dfa;
+  uint32_t off_dfas;       // DfaDesc[n_dfas + has_name_dfa]
+  uint32_t off_fields;     // FieldDesc[n_fields]
+  uint32_t off_name_field; // u32[nsets of name DFA]: set id -> field id (kNone)
+  uint32_t off_sets;       // Span[total sets]: sorted local pattern ids
+  uint32_t off_cands;      // Span[total sets]: sorted rule ids keyed on the set
+  uint32_t off_rules;      // Span[n_rules] into matchers (units of MatcherDesc)
+  uint32_t off_matchers;   // MatcherDesc[]
+  uint32_t off_pool;       // u32 pool
+  uint32_t off_tables;     // start of all DFA tables
+  uint32_t table_words;    // words of all DFA tables
+  uint32_t off_cmaps;      // (n_dfas + has_name_dfa) * 64 words of byte->class maps
+  uint32_t total_words;
+  uint32_t off_remotes;    // Span[n_rules]: sorted allowed remote ids (len 0 = any)
+  uint32_t any_remotes;    // 1 if no rule restricts the remote identity
+  Span zero_list;          // rules without matchers but with a remote set (sorted)
+  uint32_t pad[9];         // header = 32 words
+};
+static_assert(sizeof(HttpHeader) == 128, "header is 32 words");
+
+// ---------------------------------------------------------------- Kafka --
+// Rule semantics follow pkg/kafka/policy.go:144-225 and
+// pkg/policy/api/kafka.go:248-271 (after Sanitize, rule_validation.go:190-233).
+struct KafkaRuleDesc {
+  uint32_t keys_lo, keys_hi;  // apiKeyInt as a bitmask over kinds 0..63
+  uint32_t flags;             // bit0: apiKeyInt empty (any kind); bit1: version set;
+                              // bit2: topic set; bit3: clientID set
+  int32_t version;            // apiVersionInt when set
+  uint32_t client_off, client_len;  // bytes in the string area
+  uint32_t topic_off, topic_len;
+};
+constexpr uint32_t kKRuleAnyKey = 1u, kKRuleVersion = 2u, kKRuleTopic = 4u, kKRuleClient = 8u;
+
+// Open-addressed topic table: hash -> Span of rule ids (sorted) whose Topic
+// equals that string.
+struct KafkaTopicSlot {
+  uint32_t hash;      // FNV-1a 32 of the topic; 0 marks an empty slot (hash 0 remapped)
+  uint32_t str_off, str_len;
+  uint32_t list_off, list_len;
+  uint32_t pad[3];
+};
+
+struct KafkaHeader {
+  uint32_t magic;
+  uint32_t n_rules;
+  uint32_t off_rules;       // KafkaRuleDesc[n_rules]
+  uint32_t off_strings;     // byte area (word offset)
+  uint32_t off_pool;        // u32 pool
+  uint32_t off_slots;       // KafkaTopicSlot[n_slots]
+  uint32_t n_slots;         // power of two (0 when no topic rules)
+  Span notopic_by_kind[65]; // rules with Topic=="" allowing kind k (k<64), [64] = other kinds
+  Span all_by_kind[65];     // every rule allowing kind k (used when the request has no topics)
+  uint32_t total_words;
+};
+
+}  // namespace l7m

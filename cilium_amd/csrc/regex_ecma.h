@@ -1,0 +1,70 @@
+// regex_ecma.h — ECMAScript (libstdc++ std::regex dialect) parser and the
+// multi-pattern DFA builder used to compile Cilium L7 HTTP rules.
+//
+// Reference semantics: Envoy's HeaderData builds `std::regex(value,
+// std::regex::optimize)` (ECMAScript grammar) and matches with
+// `std::regex_match` (full match) — see the vendored HeaderMatcher docs
+// pkg/envoy/envoy/api/v2/route/route.pb.go:2420-2430 and the call site
+// envoy/cilium_network_policy.h:68-71.  This file restates the libstdc++
+// ECMAScript grammar (scanner/compiler of GCC 11) as an AST, lowers it to a
+// Thompson NFA and determinises a *set* of patterns into one DFA whose end
+// column reports which patterns matched.  No backtracking, no recursion on the
+// input: membership is exact for the regular subset (everything except
+// back-references, look-ahead and \b / \B, which are reported Unsupported).
+#pragma once
+#include <bitset>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace l7m {
+namespace re {
+
+using ByteSet = std::bitset<256>;
+
+enum class Status { Ok = 0, Syntax = 1, Unsupported = 2, TooBig = 3 };
+
+struct Node {
+  enum Kind : uint8_t { Empty, Set, Cat, Alt, Rep, Bol, Eol } kind = Empty;
+  ByteSet set;            // Set
+  std::vector<int> kids;  // Cat / Alt / Rep(1)
+  int min = 0, max = 0;   // Rep; max < 0 = unbounded
+};
+
+struct Ast {
+  std::vector<Node> nodes;
+  int root = -1;
+};
+
+// Parse `pat` with the libstdc++ ECMAScript grammar.  Patterns that
+// std::regex rejects are expected to be filtered by the caller first (the
+// compiler validates with std::regex itself); this parser reports Syntax for
+// anything it cannot parse and Unsupported for non-regular constructs.
+Status parse_ecma(const std::string& pat, Ast* out, std::string* err);
+
+// AST matching exactly the bytes of `lit` (Envoy HeaderMatchType::Value).
+Ast literal_ast(const std::string& lit);
+
+// One compiled DFA over a set of patterns.
+struct Dfa {
+  int ncls = 0;                 // byte classes
+  uint8_t cmap[256] = {0};      // byte -> class
+  int nstates = 0;              // state 0 is the dead state
+  int start = 0;
+  std::vector<uint32_t> next;   // nstates * ncls, next-state ids
+  std::vector<uint32_t> endset; // nstates: id into sets (0 = empty set)
+  std::vector<std::vector<uint32_t>> sets;  // set id -> sorted pattern ids
+};
+
+struct DfaLimits {
+  size_t max_states = 1u << 20;
+  size_t max_table_bytes = 64ull << 20;  // (ncls + 1) * 4 * states
+};
+
+// Determinise patterns[0..n) (pattern id = index) into one minimised DFA with
+// states numbered breadth-first from the start state.  Returns TooBig when a
+// limit is exceeded (caller splits the pattern set).
+Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, Dfa* out);
+
+}  // namespace re
+}  // namespace l7m

@@ -1,0 +1,409 @@
+"""Python binding of libl7match.so — the MI355X batched L7 policy evaluator.
+
+This module is a thin ctypes layer over the C ABI declared in
+``include/l7match.h`` (the same entry points a cgo shim would bind, see
+INTEGRATION.md).  It mirrors the reference's rule-import types
+(``api.PortRuleHTTP`` pkg/policy/api/http.go:26-58, ``api.PortRuleKafka``
+pkg/policy/api/kafka.go:26-106) and its verdict calls
+(``NetworkPolicyMap::Allowed`` envoy/cilium_network_policy.h:223,
+``(*RequestMessage).MatchesRule`` pkg/kafka/policy.go:200), batched.
+
+There is no CPU evaluation path: every verdict is computed by the HIP kernels
+in libl7match.so.  If the library is missing, importing this module fails.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libl7match.so")
+
+L7M_OK = 0
+L7M_EINVAL = -1
+L7M_EINVAL_REGEX = -2
+L7M_EINVAL_RULE = -3
+L7M_EUNSUPPORTED = -4
+L7M_ENOMEM = -5
+L7M_EDEVICE = -6
+L7M_ETOOBIG = -7
+
+VERDICT_DENY = -1
+VERDICT_PARSE_ERROR = -2
+VERDICT_UNSUPPORTED = -3
+VERDICT_ALLOW_NO_L7 = 0x7FFFFFFF
+
+DIALECT_ENVOY_ECMA_FULL = 0
+DIALECT_RE2_SEARCH = 1
+
+PROTO_HTTP = 1
+PROTO_KAFKA = 2
+
+HTTP_REC_FIXED = 20
+F_METHOD, F_PATH, F_AUTHORITY, F_INGRESS = 1, 2, 4, 8
+
+# Every symbol include/l7match.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "l7m_compile_http", "l7m_compile_kafka", "l7m_retain", "l7m_release",
+    "l7m_ruleset_get_info", "l7m_ruleset_program", "l7m_http_translate",
+    "l7m_http_record_size", "l7m_pack_http", "l7m_eval", "l7m_eval_device",
+    "l7m_alloc_pinned", "l7m_free_pinned", "l7m_abi_version", "l7m_device_count",
+)
+
+
+class L7Error(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"l7match error {code}: {msg}")
+        self.code = code
+
+
+class _HttpRule(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_char_p), ("method", ctypes.c_char_p), ("host", ctypes.c_char_p),
+                ("headers", ctypes.POINTER(ctypes.c_char_p)), ("n_headers", ctypes.c_uint32),
+                ("n_remote_ids", ctypes.c_uint32), ("remote_ids", ctypes.POINTER(ctypes.c_uint32))]
+
+
+class _KafkaRule(ctypes.Structure):
+    _fields_ = [("role", ctypes.c_char_p), ("api_key", ctypes.c_char_p),
+                ("api_version", ctypes.c_char_p), ("client_id", ctypes.c_char_p),
+                ("topic", ctypes.c_char_p)]
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("dialect", ctypes.c_uint32),
+                ("max_dfa_states", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("max_table_bytes", ctypes.c_uint64)]
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("proto", ctypes.c_uint32), ("n_rules", ctypes.c_uint32),
+                ("n_fields", ctypes.c_uint32), ("n_dfas", ctypes.c_uint32),
+                ("total_dfa_states", ctypes.c_uint64), ("program_bytes", ctypes.c_uint64),
+                ("n_counters", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class _Matcher(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("value", ctypes.c_char_p),
+                ("kind", ctypes.c_uint32), ("has_regex_flag", ctypes.c_uint32)]
+
+
+class _HttpReq(ctypes.Structure):
+    _fields_ = [("method", ctypes.c_char_p), ("path", ctypes.c_char_p),
+                ("authority", ctypes.c_char_p),
+                ("header_names", ctypes.POINTER(ctypes.c_char_p)),
+                ("header_values", ctypes.POINTER(ctypes.c_char_p)),
+                ("n_headers", ctypes.c_uint32), ("remote_id", ctypes.c_uint32),
+                ("dport", ctypes.c_uint16), ("ingress", ctypes.c_uint16)]
+
+
+def _load() -> ctypes.CDLL:
+    # PyTorch-ROCm ships its own libamdhip64 (same SONAME).  If torch is
+    # present, load it first so this process has ONE HIP runtime: our DT_NEEDED
+    # then binds to torch's copy and device buffers/streams are shared.  (If
+    # libl7match pulled /opt/rocm's copy first, torch would load a second
+    # runtime and fail with "No HIP GPUs are available".)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C cilium_amd/csrc` "
+                          "(there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    lib.l7m_compile_http.argtypes = [ctypes.POINTER(_HttpRule), sz, ctypes.POINTER(_Opts),
+                                     ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.l7m_compile_kafka.argtypes = [ctypes.POINTER(_KafkaRule), sz, ctypes.POINTER(_Opts),
+                                      ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.l7m_release.argtypes = [P]
+    lib.l7m_release.restype = None
+    lib.l7m_retain.argtypes = [P]
+    lib.l7m_retain.restype = None
+    lib.l7m_ruleset_get_info.argtypes = [P, ctypes.POINTER(_Info)]
+    lib.l7m_ruleset_program.argtypes = [P, P, ctypes.POINTER(sz)]
+    lib.l7m_http_translate.argtypes = [ctypes.POINTER(_HttpRule), ctypes.POINTER(_Matcher), sz,
+                                       ctypes.c_char_p, sz]
+    lib.l7m_http_record_size.argtypes = [ctypes.POINTER(_HttpReq)]
+    lib.l7m_http_record_size.restype = sz
+    lib.l7m_pack_http.argtypes = [ctypes.POINTER(_HttpReq), sz, P, sz, P]
+    lib.l7m_pack_http.restype = sz
+    lib.l7m_eval.argtypes = [P, P, sz, P, sz, P, P, ctypes.c_uint32]
+    lib.l7m_eval_device.argtypes = [P, P, sz, P, sz, P, P, P, ctypes.c_uint32]
+    lib.l7m_alloc_pinned.argtypes = [sz, ctypes.POINTER(P)]
+    lib.l7m_free_pinned.argtypes = [P]
+    lib.l7m_free_pinned.restype = None
+    return lib
+
+
+_lib = _load()
+
+
+def lib() -> ctypes.CDLL:
+    return _lib
+
+
+def device_count() -> int:
+    return int(_lib.l7m_device_count())
+
+
+def kafka_available() -> bool:
+    try:
+        RuleSet.compile_kafka([])
+        return True
+    except L7Error as e:
+        if e.code == L7M_EUNSUPPORTED:
+            return False
+        raise
+
+
+def _b(s: Optional[str]) -> Optional[bytes]:
+    if s is None:
+        return None
+    return s.encode("utf-8", "surrogateescape") if isinstance(s, str) else bytes(s)
+
+
+# --------------------------------------------------------------------------
+# Reference rule types
+# --------------------------------------------------------------------------
+@dataclass
+class PortRuleHTTP:
+    """api.PortRuleHTTP (pkg/policy/api/http.go:26-58). Empty string = unset."""
+    Path: str = ""
+    Method: str = ""
+    Host: str = ""
+    Headers: Sequence[str] = field(default_factory=list)
+    # allowed_remotes_ of the enclosing PortNetworkPolicyRule (NPDS
+    # remote_policies, envoy/cilium_network_policy.h:90-97); empty = any.
+    RemoteIDs: Sequence[int] = field(default_factory=list)
+
+
+@dataclass
+class PortRuleKafka:
+    """api.PortRuleKafka (pkg/policy/api/kafka.go:26-106). Empty string = unset."""
+    Role: str = ""
+    APIKey: str = ""
+    APIVersion: str = ""
+    ClientID: str = ""
+    Topic: str = ""
+
+
+@dataclass
+class HeaderMatcher:
+    """envoy_api_v2_route.HeaderMatcher as emitted by getHTTPRule."""
+    Name: str
+    Value: str = ""
+    Regex: Optional[bool] = None  # None = nil BoolValue
+
+    @property
+    def kind(self) -> str:
+        return "present" if not self.Value else ("regex" if self.Regex else "value")
+
+
+@dataclass
+class HTTPRequest:
+    """One HTTP request head as Envoy's HeaderMap presents it."""
+    method: Optional[str] = "GET"
+    path: Optional[str] = "/"
+    authority: Optional[str] = None
+    headers: Sequence[Tuple[str, str]] = ()
+    remote_id: int = 0
+    dport: int = 80
+    ingress: bool = True
+
+
+def _http_rule_struct(r: PortRuleHTTP, keep: list) -> _HttpRule:
+    hs = [_b(h) for h in r.Headers]
+    arr = (ctypes.c_char_p * max(1, len(hs)))(*hs)
+    rem = (ctypes.c_uint32 * max(1, len(r.RemoteIDs)))(*list(r.RemoteIDs))
+    keep += [arr, rem]
+    return _HttpRule(_b(r.Path) or None, _b(r.Method) or None, _b(r.Host) or None,
+                     ctypes.cast(arr, ctypes.POINTER(ctypes.c_char_p)), len(hs),
+                     len(r.RemoteIDs), ctypes.cast(rem, ctypes.POINTER(ctypes.c_uint32)))
+
+
+def get_http_rule(r: PortRuleHTTP) -> List[HeaderMatcher]:
+    """getHTTPRule (pkg/envoy/server.go:261-320) as computed by libl7match."""
+    keep: list = []
+    st = _http_rule_struct(r, keep)
+    out = (_Matcher * 256)()
+    err = ctypes.create_string_buffer(512)
+    n = _lib.l7m_http_translate(ctypes.byref(st), out, 256, err, 512)
+    if n < 0:
+        raise L7Error(n, err.value.decode())
+    res = []
+    for i in range(n):
+        m = out[i]
+        res.append(HeaderMatcher(m.name.decode(), (m.value or b"").decode(),
+                                 True if m.has_regex_flag else None))
+    return res
+
+
+# --------------------------------------------------------------------------
+# Arena packing
+# --------------------------------------------------------------------------
+def pack_http(reqs: Sequence[HTTPRequest]) -> Tuple[np.ndarray, np.ndarray]:
+    """Pack requests into (arena uint8[], offsets uint64[]) via l7m_pack_http."""
+    keep: list = []
+    arr = (_HttpReq * max(1, len(reqs)))()
+    total = 0
+    for i, q in enumerate(reqs):
+        names = (ctypes.c_char_p * max(1, len(q.headers)))(*[_b(h[0]) for h in q.headers])
+        vals = (ctypes.c_char_p * max(1, len(q.headers)))(*[_b(h[1]) for h in q.headers])
+        keep += [names, vals]
+        arr[i] = _HttpReq(_b(q.method), _b(q.path), _b(q.authority),
+                          ctypes.cast(names, ctypes.POINTER(ctypes.c_char_p)),
+                          ctypes.cast(vals, ctypes.POINTER(ctypes.c_char_p)),
+                          len(q.headers), q.remote_id, q.dport, 1 if q.ingress else 0)
+        sz = _lib.l7m_http_record_size(ctypes.byref(arr[i]))
+        if sz == 0:
+            raise L7Error(L7M_EINVAL, f"request {i} is not encodable")
+        total += sz
+    arena = np.zeros(max(4, total), dtype=np.uint8)
+    offs = np.zeros(len(reqs), dtype=np.uint64)
+    if reqs:
+        used = _lib.l7m_pack_http(arr, len(reqs), arena.ctypes.data, arena.nbytes, offs.ctypes.data)
+        if used != total:
+            raise L7Error(L7M_EINVAL, "pack failed")
+    return arena, offs
+
+
+def pack_records(records: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    """Pack pre-encoded records (e.g. Kafka wire requests), 4-byte aligned."""
+    offs = np.zeros(len(records), dtype=np.uint64)
+    total = 0
+    for i, r in enumerate(records):
+        offs[i] = total
+        total += (len(r) + 3) & ~3
+    arena = np.zeros(max(4, total), dtype=np.uint8)
+    for i, r in enumerate(records):
+        o = int(offs[i])
+        arena[o:o + len(r)] = np.frombuffer(r, dtype=np.uint8)
+    return arena, offs
+
+
+# --------------------------------------------------------------------------
+# Rule sets
+# --------------------------------------------------------------------------
+class RuleSet:
+    """An immutable compiled rule set (refcounted handle in libl7match)."""
+
+    def __init__(self, handle: int, proto: int):
+        self._h = ctypes.c_void_p(handle)
+        self.proto = proto
+        info = _Info()
+        _lib.l7m_ruleset_get_info(self._h, ctypes.byref(info))
+        self.info = info
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.l7m_release(h)
+            self._h = ctypes.c_void_p(0)
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    @property
+    def n_rules(self) -> int:
+        return int(self.info.n_rules)
+
+    @property
+    def n_counters(self) -> int:
+        return int(self.info.n_counters)
+
+    def program(self) -> np.ndarray:
+        n = ctypes.c_size_t(0)
+        _lib.l7m_ruleset_program(self._h, None, ctypes.byref(n))
+        buf = np.zeros(n.value // 4, dtype=np.uint32)
+        _lib.l7m_ruleset_program(self._h, buf.ctypes.data, ctypes.byref(n))
+        return buf
+
+    @staticmethod
+    def _opts(dialect: int, max_dfa_states: int, max_table_bytes: int) -> _Opts:
+        return _Opts(ctypes.sizeof(_Opts), dialect, max_dfa_states, 0, max_table_bytes)
+
+    @classmethod
+    def compile_http(cls, rules: Sequence[PortRuleHTTP], dialect: int = DIALECT_ENVOY_ECMA_FULL,
+                     max_dfa_states: int = 0, max_table_bytes: int = 0) -> "RuleSet":
+        keep: list = []
+        arr = (_HttpRule * max(1, len(rules)))(*[_http_rule_struct(r, keep) for r in rules])
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        opts = cls._opts(dialect, max_dfa_states, max_table_bytes)
+        rc = _lib.l7m_compile_http(arr, len(rules), ctypes.byref(opts), ctypes.byref(out), err, 1024)
+        if rc != L7M_OK:
+            raise L7Error(rc, err.value.decode(errors="replace"))
+        return cls(out.value, PROTO_HTTP)
+
+    @classmethod
+    def compile_kafka(cls, rules: Sequence[PortRuleKafka]) -> "RuleSet":
+        arr = (_KafkaRule * max(1, len(rules)))(*[
+            _KafkaRule(_b(r.Role) or None, _b(r.APIKey) or None, _b(r.APIVersion) or None,
+                       _b(r.ClientID) or None, _b(r.Topic) or None) for r in rules])
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        opts = cls._opts(0, 0, 0)
+        rc = _lib.l7m_compile_kafka(arr, len(rules), ctypes.byref(opts), ctypes.byref(out), err, 1024)
+        if rc != L7M_OK:
+            raise L7Error(rc, err.value.decode(errors="replace"))
+        return cls(out.value, PROTO_KAFKA)
+
+    # ---- evaluation -------------------------------------------------------
+    def eval(self, arena: np.ndarray, offsets: np.ndarray, hits: Optional[np.ndarray] = None
+             ) -> np.ndarray:
+        """Host buffers -> int32 verdicts (H2D, kernel, D2H on the current device)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.shape[0]
+        verdicts = np.empty(n, dtype=np.int32)
+        hp = None
+        if hits is not None:
+            assert hits.dtype == np.uint64 and hits.shape[0] >= self.n_counters
+            hp = hits.ctypes.data
+        rc = _lib.l7m_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data, n,
+                           verdicts.ctypes.data, hp, 0)
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_eval failed")
+        return verdicts
+
+    def eval_device(self, d_arena, arena_bytes: int, d_offsets, n: int, d_verdicts,
+                    d_hits=None, stream=None) -> None:
+        """Device pointers (ints or torch tensors) -> enqueue on `stream` (int handle)."""
+        def ptr(x):
+            if x is None:
+                return None
+            return x.data_ptr() if hasattr(x, "data_ptr") else int(x)
+        rc = _lib.l7m_eval_device(self._h, ptr(d_arena), arena_bytes, ptr(d_offsets), n,
+                                  ptr(d_verdicts), ptr(d_hits), stream, 0)
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_eval_device failed")
+
+
+class NetworkPolicyMap:
+    """Batched mirror of Envoy's NetworkPolicyMap::Allowed for one port policy
+    (envoy/cilium_network_policy.h:223-237): Allowed(requests) -> bool[]."""
+
+    def __init__(self, rules: Sequence[PortRuleHTTP]):
+        self.ruleset = RuleSet.compile_http(rules)
+
+    def verdicts(self, reqs: Sequence[HTTPRequest]) -> np.ndarray:
+        arena, offs = pack_http(reqs)
+        return self.ruleset.eval(arena, offs)
+
+    def Allowed(self, reqs: Sequence[HTTPRequest]) -> np.ndarray:
+        v = self.verdicts(reqs)
+        return (v >= 0)
+
+
+def matches_rule(records: Sequence[bytes], rules: Sequence[PortRuleKafka]) -> np.ndarray:
+    """Batched (*RequestMessage).MatchesRule (pkg/kafka/policy.go:200) over raw
+    wire requests as proto.ReadReq returns them; returns int32 verdicts."""
+    rs = RuleSet.compile_kafka(rules)
+    arena, offs = pack_records(records)
+    return rs.eval(arena, offs)

@@ -1,0 +1,219 @@
+/*
+ * l7match.h — C ABI of libl7match.so, the MI355X-native batched L7 policy
+ * evaluator for Cilium's L7 rule model (PortRuleHTTP / PortRuleKafka).
+ *
+ * This is the drop-in boundary.  Each entry point replaces one reference
+ * interface (all paths relative to the uniberg/cilium tree):
+ *
+ *   l7m_compile_http   replaces the rule-import half of the HTTP path:
+ *                      getHTTPRule  pkg/envoy/server.go:261-320  (PortRuleHTTP ->
+ *                      HeaderMatcher list) followed by the std::regex construction
+ *                      in Envoy's HeaderData (envoy/cilium_network_policy.h:52-66,
+ *                      policy instantiation envoy/cilium_network_policy.cc:63-65).
+ *                      A regex that std::regex rejects makes the call fail
+ *                      (L7M_EINVAL_REGEX) exactly where Envoy would NACK the
+ *                      policy; the caller keeps its previous handle.
+ *   l7m_compile_kafka  replaces PortRuleKafka.Sanitize
+ *                      (pkg/policy/api/rule_validation.go:190-233) applied to the
+ *                      rule slice handed to MatchesRule (pkg/kafka/policy.go:200).
+ *   l7m_eval           replaces, for a batch of N requests,
+ *                        HTTP : NetworkPolicyMap::Allowed
+ *                               envoy/cilium_network_policy.h:223-237 (-> :198-203,
+ *                               :169-192, :128-146, :90-108, :68-71)
+ *                        Kafka: kafka.ReadRequest pkg/kafka/request.go:186-229 +
+ *                               (*RequestMessage).MatchesRule pkg/kafka/policy.go:200-225
+ *                      The reference returns a bare bool per request; this ABI
+ *                      returns an int32 verdict per request (see L7M_VERDICT_*):
+ *                      -1 deny, i >= 0 allow decided by rule i (input order).
+ *   l7m_eval_device    the same on buffers already resident in HBM, enqueued on a
+ *                      caller-provided HIP stream (no host synchronisation).
+ *
+ * Conventions: every int-returning function returns L7M_OK (0) or a negative
+ * L7M_E* code.  When err != NULL and errlen > 0 a NUL-terminated message is
+ * written on failure.  Handles are immutable after compile and reference
+ * counted; l7m_eval / l7m_eval_device are reentrant and may be called
+ * concurrently from many threads on the same handle (each call uses its own
+ * stream and scratch), mirroring Envoy's lock-free per-worker read path.
+ *
+ * Nothing in this header depends on HIP or torch types: streams are passed
+ * as void* (hipStream_t), device buffers as void*.
+ */
+#ifndef L7MATCH_H
+#define L7MATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define L7M_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define L7M_OK 0
+#define L7M_EINVAL (-1)         /* bad argument (NULL pointer, bad size)          */
+#define L7M_EINVAL_REGEX (-2)   /* std::regex would throw: Envoy NACKs the policy */
+#define L7M_EINVAL_RULE (-3)    /* Sanitize() error / getHTTPRule sort panic      */
+#define L7M_EUNSUPPORTED (-4)   /* valid regex outside the compiled subset        */
+#define L7M_ENOMEM (-5)         /* host or device allocation failed               */
+#define L7M_EDEVICE (-6)        /* HIP runtime error / no device                  */
+#define L7M_ETOOBIG (-7)        /* rule set exceeds a compile-time limit          */
+
+/* ---- verdicts (int32 per request) --------------------------------------- */
+#define L7M_VERDICT_DENY (-1)         /* no rule allows the request               */
+#define L7M_VERDICT_PARSE_ERROR (-2)  /* Kafka: ReadRequest would return an error  */
+#define L7M_VERDICT_UNSUPPORTED (-3)  /* Kafka: compressed message set (gzip/snappy) */
+#define L7M_VERDICT_ALLOW_NO_L7 (0x7fffffff) /* HTTP rule list empty: port has no L7
+                                        rules, Envoy allows (cilium_network_policy.h:129-135) */
+
+/* ---- dialects ------------------------------------------------------------ */
+#define L7M_DIALECT_ENVOY_ECMA_FULL 0 /* std::regex ECMAScript, regex_match (full)  */
+#define L7M_DIALECT_RE2_SEARCH 1      /* reserved: RE2 unanchored search (not yet)  */
+
+#define L7M_PROTO_HTTP 1
+#define L7M_PROTO_KAFKA 2
+
+typedef struct l7m_ruleset l7m_ruleset; /* opaque */
+
+/* Verbatim api.PortRuleHTTP (pkg/policy/api/http.go:26-58).  NULL or "" = unset.
+ * remote_ids: allowed_remotes_ of the PortNetworkPolicyRule this HTTP rule
+ * belongs to (envoy/cilium_network_policy.h:90-97, NPDS remote_policies);
+ * n_remote_ids == 0 means any remote identity.  A request is allowed by rule i
+ * iff its remote_id is in the set AND every matcher of the rule holds. */
+typedef struct {
+  const char* path;
+  const char* method;
+  const char* host;
+  const char* const* headers; /* "Name: value" (literal) or "Name" (presence) */
+  uint32_t n_headers;
+  uint32_t n_remote_ids;
+  const uint32_t* remote_ids;
+} l7m_http_rule;
+
+/* Verbatim api.PortRuleKafka (pkg/policy/api/kafka.go:26-106).  NULL or "" = unset. */
+typedef struct {
+  const char* role;
+  const char* api_key;
+  const char* api_version;
+  const char* client_id;
+  const char* topic;
+} l7m_kafka_rule;
+
+typedef struct {
+  uint32_t struct_size;     /* sizeof(l7m_opts); 0 = use defaults               */
+  uint32_t dialect;         /* L7M_DIALECT_*                                    */
+  uint32_t max_dfa_states;  /* per DFA group before splitting (0 = default)     */
+  uint32_t flags;           /* reserved, 0                                      */
+  uint64_t max_table_bytes; /* per DFA group before splitting (0 = default)     */
+} l7m_opts;
+
+typedef struct {
+  uint32_t proto;           /* L7M_PROTO_*                                       */
+  uint32_t n_rules;
+  uint32_t n_fields;        /* HTTP: distinct header fields referenced          */
+  uint32_t n_dfas;          /* HTTP: DFA groups (incl. the header-name DFA)     */
+  uint64_t total_dfa_states;
+  uint64_t program_bytes;   /* size of the device program blob                  */
+  uint32_t n_counters;      /* length of rule_hits arrays = n_rules + 2         */
+  uint32_t reserved;
+} l7m_ruleset_info;
+
+/* ---- rule compilation (cold path) ---------------------------------------- */
+int l7m_compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts* opts,
+                     l7m_ruleset** out, char* err, size_t errlen);
+int l7m_compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts* opts,
+                      l7m_ruleset** out, char* err, size_t errlen);
+void l7m_retain(l7m_ruleset* rs);
+void l7m_release(l7m_ruleset* rs);
+int l7m_ruleset_get_info(const l7m_ruleset* rs, l7m_ruleset_info* out);
+/* Copy of the packed device program (for inspection / tests).  *len receives
+ * the size; when buf is NULL only the size is returned. */
+int l7m_ruleset_program(const l7m_ruleset* rs, void* buf, size_t* len);
+
+/* getHTTPRule translation of one rule (pkg/envoy/server.go:261-320), sorted as
+ * SortHeaderMatchers (pkg/envoy/sort.go:205-250).  Writes up to cap matchers;
+ * returns the number of matchers (>= 0) or a negative status.  kind: 0 regex,
+ * 1 literal value, 2 presence (Envoy HeaderMatchType Regex/Value/Present). Name
+ * and value pointers stay valid until the next call on the same thread. */
+typedef struct {
+  const char* name;  /* as in the NPDS HeaderMatcher (not lower-cased)           */
+  const char* value;
+  uint32_t kind;
+  uint32_t has_regex_flag; /* HeaderMatcher.Regex != nil                        */
+} l7m_header_matcher;
+int l7m_http_translate(const l7m_http_rule* rule, l7m_header_matcher* out, size_t cap,
+                       char* err, size_t errlen);
+
+/* ---- request arena --------------------------------------------------------
+ * A batch is a byte arena holding N records plus an array of N uint64 byte
+ * offsets (each record 4-byte aligned).
+ *
+ * HTTP record (little endian), L7M_HTTP_REC_FIXED bytes of fixed header:
+ *   u32 rec_len        bytes of this record, unpadded (>= 20 + 4*n_hdr)
+ *   u32 remote_id      source security identity (Envoy remote_id)
+ *   u16 dport          destination port
+ *   u8  flags          L7M_HTTP_F_*
+ *   u8  n_hdr          number of regular headers
+ *   u16 method_len, u16 path_len, u16 authority_len, u16 reserved
+ *   n_hdr x { u16 name_len, u16 value_len }           header directory
+ *   method | path | authority | name0 | value0 | name1 | value1 | ...
+ * Header names must already be lower case (Envoy's codec lower-cases them);
+ * the first occurrence of a name is the one matched (HeaderMap::get).
+ *
+ * Kafka record: the request exactly as proto.ReadReq returns it
+ * (vendor/github.com/optiopay/kafka/proto/messages.go:124-165): big-endian
+ * int32 size followed by size bytes; record length = 4 + size.
+ */
+#define L7M_HTTP_REC_FIXED 20
+#define L7M_HTTP_F_METHOD 0x01
+#define L7M_HTTP_F_PATH 0x02
+#define L7M_HTTP_F_AUTHORITY 0x04
+#define L7M_HTTP_F_INGRESS 0x08
+
+typedef struct {
+  const char* method;    /* NULL = absent */
+  const char* path;      /* NULL = absent */
+  const char* authority; /* NULL = absent */
+  const char* const* header_names;  /* lower-cased by the packer */
+  const char* const* header_values;
+  uint32_t n_headers;
+  uint32_t remote_id;
+  uint16_t dport;
+  uint16_t ingress;
+} l7m_http_request;
+
+/* Bytes one request occupies in the arena (4-byte padded); 0 if not encodable. */
+size_t l7m_http_record_size(const l7m_http_request* req);
+/* Pack n requests; writes offsets[i]; returns bytes used or 0 on overflow. */
+size_t l7m_pack_http(const l7m_http_request* reqs, size_t n, uint8_t* arena, size_t cap,
+                     uint64_t* offsets);
+
+/* ---- evaluation (hot path) ----------------------------------------------
+ * verdicts: int32[n].  rule_hits: NULL or uint64[n_rules + 2], ACCUMULATED
+ * (not cleared): [0] denies, [1] parse errors + unsupported, [2 + i] requests
+ * allowed by rule i.  flags: reserved, 0.
+ */
+int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
+             const uint64_t* rec_offsets, size_t n, int32_t* verdicts, uint64_t* rule_hits,
+             uint32_t flags);
+
+/* Device-resident variant: all pointers are device pointers on the current HIP
+ * device; the work is enqueued on `hip_stream` (NULL = default stream) and the
+ * call returns without synchronising. */
+int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes,
+                    const void* d_rec_offsets, size_t n, void* d_verdicts, void* d_rule_hits,
+                    void* hip_stream, uint32_t flags);
+
+/* Pinned host memory helpers (cgo may not retain Go pointers across calls). */
+int l7m_alloc_pinned(size_t bytes, void** out);
+void l7m_free_pinned(void* p);
+
+/* Library / device information. */
+int l7m_abi_version(void);
+int l7m_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* L7MATCH_H */

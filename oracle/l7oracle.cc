@@ -1,0 +1,668 @@
+// l7oracle.cc — CPU ORACLE for the L7 verdict path.  TEST INFRASTRUCTURE ONLY.
+//
+// This is a plain restatement of the reference algorithm, used by tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.  The
+// product (libl7match.so) never links, loads or calls it.
+//
+// HTTP (dialect envoy-ecma-full):
+//   getHTTPRule            pkg/envoy/server.go:261-320
+//   SortHeaderMatchers     pkg/envoy/sort.go:205-250 (panic on nil Regex -> error)
+//   HeaderData / matchHeaders (Envoy @ envoy/WORKSPACE:10, called from
+//                          envoy/cilium_network_policy.h:68-71): lower-cased name,
+//                          first header with that name, std::regex_match for
+//                          regex (ECMAScript | optimize, the engine Envoy links),
+//                          == for literal values, presence otherwise.
+//   OR over rules          envoy/cilium_network_policy.h:98-105 (first index reported)
+//   no HTTP rules -> allow envoy/cilium_network_policy.h:129-135
+// Kafka:
+//   Sanitize               pkg/policy/api/rule_validation.go:190-233,
+//                          MapRoleToAPIKey pkg/policy/api/kafka.go:274-293
+//   ReadReq / ReadRequest  vendor/github.com/optiopay/kafka/proto/messages.go:124-165,
+//                          pkg/kafka/request.go:186-229 and the per-kind readers
+//                          (messages.go:357-482, 493-522, 752-809, 1018-1039,
+//                          1158-1213, 1374-1411, 1572-1628, 1791-1839),
+//                          decoder semantics serialization.go:30-196, utils.go:9-24
+//   MatchesRule            pkg/kafka/policy.go:27-225
+// Verdict encoding matches include/l7match.h (-1 deny, i >= 0 deciding rule).
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <regex>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_set>
+#include <vector>
+
+#include "../include/l7match.h"
+
+namespace {
+
+void set_err(char* err, size_t errlen, const std::string& m) {
+  if (!err || !errlen) return;
+  size_t k = m.size() < errlen - 1 ? m.size() : errlen - 1;
+  memcpy(err, m.data(), k);
+  err[k] = 0;
+}
+std::string S(const char* p) { return p ? std::string(p) : std::string(); }
+
+// ============================================================== HTTP ====
+struct Matcher {
+  std::string name, value;
+  bool has_regex;  // Regex != nil
+};
+struct HeaderData {
+  std::string lname;
+  int kind;  // 0 regex, 1 value, 2 present
+  std::string value;
+  std::regex re;
+};
+struct HttpOracle {
+  std::vector<std::vector<HeaderData>> rules;
+  std::vector<std::unordered_set<uint32_t>> remotes;  // allowed_remotes_ (empty = any)
+};
+
+bool hm_less(const Matcher& a, const Matcher& b) {
+  if (a.name != b.name) return a.name < b.name;
+  if (a.value != b.value) return a.value < b.value;
+  return !a.has_regex && b.has_regex;  // only reached for regex/regex pairs
+}
+
+// Parsed record view.
+struct HttpReq {
+  bool ok = false;
+  std::vector<std::pair<std::string, std::string>> headers;  // pseudo first
+  uint32_t remote_id = 0;
+};
+
+HttpReq parse_http(const uint8_t* arena, size_t arena_bytes, uint64_t off) {
+  HttpReq q;
+  if ((off & 3) || off + L7M_HTTP_REC_FIXED > arena_bytes) return q;
+  const uint8_t* r = arena + off;
+  uint32_t w[5];
+  memcpy(w, r, sizeof w);
+  uint32_t len = w[0], flags = (w[2] >> 16) & 0xff, nh = w[2] >> 24;
+  uint32_t ml = w[3] & 0xffff, pl = w[3] >> 16, al = w[4] & 0xffff;
+  if (off + ((uint64_t(len) + 3) & ~3ull) > arena_bytes) return q;
+  uint64_t need = L7M_HTTP_REC_FIXED + 4ull * nh + ml + pl + al;
+  if (need > len) return q;
+  std::vector<std::pair<uint32_t, uint32_t>> dir(nh);
+  for (uint32_t j = 0; j < nh; ++j) {
+    uint32_t e;
+    memcpy(&e, r + L7M_HTTP_REC_FIXED + 4 * j, 4);
+    dir[j] = {e & 0xffff, e >> 16};
+    need += dir[j].first + dir[j].second;
+  }
+  if (need != len) return q;
+  q.remote_id = w[1];
+  size_t p = L7M_HTTP_REC_FIXED + 4ull * nh;
+  auto take = [&](uint32_t l) {
+    std::string s(reinterpret_cast<const char*>(r + p), l);
+    p += l;
+    return s;
+  };
+  std::string m = take(ml), pa = take(pl), au = take(al);
+  if (flags & L7M_HTTP_F_METHOD) q.headers.push_back({":method", m});
+  if (flags & L7M_HTTP_F_PATH) q.headers.push_back({":path", pa});
+  if (flags & L7M_HTTP_F_AUTHORITY) q.headers.push_back({":authority", au});
+  for (auto& d : dir) {
+    std::string n = take(d.first), v = take(d.second);
+    if (!n.empty() && n[0] == ':') continue;  // record contract: no pseudo names here
+    q.headers.push_back({n, v});
+  }
+  q.ok = true;
+  return q;
+}
+
+int32_t eval_http_one(const HttpOracle& o, const HttpReq& q) {
+  if (!q.ok) return L7M_VERDICT_PARSE_ERROR;
+  if (o.rules.empty()) return L7M_VERDICT_ALLOW_NO_L7;
+  for (size_t i = 0; i < o.rules.size(); ++i) {
+    // PortNetworkPolicyRule::Matches: remote id first (cilium_network_policy.h:90-97)
+    if (!o.remotes[i].empty() && !o.remotes[i].count(q.remote_id)) continue;
+    bool all = true;
+    for (const auto& hd : o.rules[i]) {
+      const std::string* v = nullptr;
+      for (const auto& h : q.headers)
+        if (h.first == hd.lname) {
+          v = &h.second;
+          break;
+        }
+      if (!v) { all = false; break; }
+      if (hd.kind == 0 && !std::regex_match(*v, hd.re)) { all = false; break; }
+      if (hd.kind == 1 && *v != hd.value) { all = false; break; }
+    }
+    if (all) return static_cast<int32_t>(i);
+  }
+  return L7M_VERDICT_DENY;
+}
+
+// ============================================================= Kafka ====
+struct KRule {
+  std::vector<int16_t> keys;  // apiKeyInt
+  bool has_version = false;
+  int16_t version = 0;
+  std::string client, topic;
+};
+struct KafkaOracle {
+  std::vector<KRule> rules;
+};
+
+const std::map<std::string, int16_t>& api_key_map() {
+  static const std::map<std::string, int16_t> m = {
+      {"produce", 0}, {"fetch", 1}, {"offsets", 2}, {"metadata", 3}, {"leaderandisr", 4},
+      {"stopreplica", 5}, {"updatemetadata", 6}, {"controlledshutdown", 7}, {"offsetcommit", 8},
+      {"offsetfetch", 9}, {"findcoordinator", 10}, {"joingroup", 11}, {"heartbeat", 12},
+      {"leavegroup", 13}, {"syncgroup", 14}, {"describegroups", 15}, {"listgroups", 16},
+      {"saslhandshake", 17}, {"apiversions", 18}, {"createtopics", 19}, {"deletetopics", 20},
+      {"deleterecords", 21}, {"initproducerid", 22}, {"offsetforleaderepoch", 23},
+      {"addpartitionstotxn", 24}, {"addoffsetstotxn", 25}, {"endtxn", 26},
+      {"writetxnmarkers", 27}, {"txnoffsetcommit", 28}, {"describeacls", 29},
+      {"createacls", 30}, {"deleteacls", 31}, {"describeconfigs", 32}, {"alterconfigs", 33}};
+  return m;
+}
+
+// Go strings.ToLower for the inputs that can matter here: ASCII, plus the two
+// non-ASCII runes that lower-case to ASCII (U+0130 -> 'i', U+212A -> 'k').
+std::string go_lower(const std::string& s) {
+  std::string r;
+  for (size_t i = 0; i < s.size();) {
+    unsigned char c = s[i];
+    if (c == 0xC4 && i + 1 < s.size() && (unsigned char)s[i + 1] == 0xB0) { r += 'i'; i += 2; continue; }
+    if (c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x84 && (unsigned char)s[i + 2] == 0xAA) {
+      r += 'k'; i += 3; continue;
+    }
+    r += (c >= 'A' && c <= 'Z') ? char(c - 'A' + 'a') : char(c);
+    ++i;
+  }
+  return r;
+}
+
+// strconv.ParseInt(s, 10, 16)
+bool go_parse_int16(const std::string& s, int16_t* out) {
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; }
+  if (i >= s.size()) return false;
+  long long v = 0;
+  for (; i < s.size(); ++i) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (s[i] - '0');
+    if (v > 40000) v = 40000;
+  }
+  if (neg) v = -v;
+  if (v < -32768 || v > 32767) return false;
+  *out = static_cast<int16_t>(v);
+  return true;
+}
+
+bool topic_chars_ok(const std::string& t) {  // ^[a-zA-Z0-9\\._\\-]+$ (Go regexp)
+  if (t.empty()) return false;
+  for (unsigned char c : t) {
+    bool ok = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') ||
+              c == '\\' || c == '.' || c == '_' || c == '-';
+    if (!ok) return false;
+  }
+  return true;
+}
+
+int sanitize(const l7m_kafka_rule& in, KRule* r, std::string* err) {
+  std::string role = S(in.role), key = S(in.api_key), ver = S(in.api_version);
+  r->client = S(in.client_id);
+  r->topic = S(in.topic);
+  if (!key.empty() && !role.empty()) { *err = "Cannot set both Role and APIKey together"; return L7M_EINVAL_RULE; }
+  if (!key.empty()) {
+    auto it = api_key_map().find(go_lower(key));
+    if (it == api_key_map().end()) { *err = "invalid Kafka APIKey"; return L7M_EINVAL_RULE; }
+    r->keys.push_back(it->second);
+  }
+  if (!role.empty()) {
+    std::string lr = go_lower(role);
+    if (lr == "produce") r->keys = {0, 3, 18};
+    else if (lr == "consume") r->keys = {1, 2, 3, 8, 9, 10, 11, 12, 13, 14, 18};
+    else { *err = "invalid Kafka APIRole"; return L7M_EINVAL_RULE; }
+  }
+  if (!ver.empty()) {
+    if (!go_parse_int16(ver, &r->version)) { *err = "invalid Kafka APIVersion"; return L7M_EINVAL_RULE; }
+    r->has_version = true;
+  }
+  if (!r->topic.empty()) {
+    if (r->topic.size() > 255) { *err = "kafka topic exceeds maximum len of 255"; return L7M_EINVAL_RULE; }
+    if (!topic_chars_ok(r->topic)) { *err = "invalid Kafka Topic name"; return L7M_EINVAL_RULE; }
+  }
+  return L7M_OK;
+}
+
+// ---- decoder with the optiopay error semantics --------------------------
+const int64_t kMaxParseBuf = 100LL * 65535;  // maxParseBufSize
+
+struct Reader {  // bytes.Reader / LimitReader view over a byte range
+  const uint8_t* p;
+  size_t len, pos = 0;
+  size_t avail() const { return len - pos; }
+};
+
+struct Dec {
+  Reader* r;
+  bool err = false;
+  bool read(uint8_t* out, size_t n) {  // io.ReadFull
+    if (r->avail() < n) {
+      r->pos = r->len;  // ReadFull consumes what is there before failing
+      return false;
+    }
+    if (out) memcpy(out, r->p + r->pos, n);
+    r->pos += n;
+    return true;
+  }
+  int64_t be(size_t n) {
+    if (err) return 0;
+    uint8_t b[8];
+    if (!read(b, n)) { err = true; return 0; }
+    uint64_t v = 0;
+    for (size_t i = 0; i < n; ++i) v = (v << 8) | b[i];
+    if (n == 1) return (int8_t)v;
+    if (n == 2) return (int16_t)v;
+    if (n == 4) return (int32_t)v;
+    return (int64_t)v;
+  }
+  int8_t i8() { return (int8_t)be(1); }
+  int16_t i16() { return (int16_t)be(2); }
+  int32_t i32() { return (int32_t)be(4); }
+  int64_t i64() { return be(8); }
+  uint32_t u32() { return (uint32_t)be(4); }
+  std::string str() {
+    if (err) return "";
+    int16_t n = i16();
+    if (err || n < 1) return "";
+    std::string s(n, '\0');
+    if (!read(reinterpret_cast<uint8_t*>(&s[0]), n)) { err = true; return ""; }
+    return s;
+  }
+  // DecodeBytes; *alloc_err set when allocParseBuf fails
+  bool bytes(std::string* out) {
+    if (err) return false;
+    int32_t n = i32();
+    if (err || n < 1) return false;
+    if (n > kMaxParseBuf) { err = true; return false; }
+    std::string s(n, '\0');
+    if (!read(reinterpret_cast<uint8_t*>(&s[0]), n)) { err = true; return false; }
+    if (out) *out = s;
+    return true;
+  }
+  // DecodeArrayLen: returns false on ErrInvalidArrayLen
+  bool arraylen(int64_t* n) {
+    int32_t v = i32();
+    if (v < 0 || v > kMaxParseBuf) return false;
+    *n = v;
+    return true;
+  }
+};
+
+uint32_t crc32_ieee(const uint8_t* p, size_t n) {
+  static uint32_t tbl[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      tbl[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = 0xffffffffu;
+  for (size_t i = 0; i < n; ++i) c = tbl[(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return c ^ 0xffffffffu;
+}
+
+enum MsRc { MS_OK, MS_ERR, MS_UNSUPPORTED };
+
+// readMessageSet(r, size, version): reads at most `size` bytes of `outer`.
+MsRc read_message_set(Reader* outer, int32_t size, int16_t version) {
+  if (size < 0 || size > kMaxParseBuf) return MS_ERR;
+  size_t lim = outer->avail() < (size_t)size ? outer->avail() : (size_t)size;
+  Reader rd{outer->p + outer->pos, lim, 0};
+  auto done = [&]() { outer->pos += rd.pos; };
+  Dec dec{&rd};
+  for (;;) {
+    dec.i64();
+    if (dec.err) { done(); return MS_OK; }   // EOF / ErrUnexpectedEOF
+    int32_t msz = dec.i32();
+    if (dec.err) { done(); return MS_OK; }
+    if (msz <= 0) { done(); return MS_OK; }
+    if (msz > kMaxParseBuf) { done(); return MS_ERR; }
+    if (rd.avail() < (size_t)msz) { rd.pos = rd.len; done(); return MS_OK; }
+    const uint8_t* mb = rd.p + rd.pos;
+    rd.pos += msz;
+    Reader mr{mb, (size_t)msz, 0};
+    Dec md{&mr};
+    uint32_t crc = md.u32();
+    if (msz <= 4) { done(); return MS_OK; }
+    if (crc != crc32_ieee(mb + 4, msz - 4)) { done(); return MS_OK; }
+    md.i8();
+    int8_t attr = md.i8();
+    if (version >= 1) md.i64();
+    int comp = attr & 3;
+    if (comp == 0) {
+      md.bytes(nullptr);
+      md.bytes(nullptr);
+      if (md.err) { done(); return MS_ERR; }
+    } else if (comp == 1 || comp == 2) {
+      md.bytes(nullptr);
+      md.bytes(nullptr);
+      if (md.err) { done(); return MS_ERR; }
+      done();
+      return MS_UNSUPPORTED;  // gzip / snappy payload: not evaluated
+    } else {
+      done();
+      return MS_OK;  // `return nil, err` with err == nil (messages.go:479-480)
+    }
+  }
+}
+
+struct KReq {
+  int32_t status = 0;  // 0 ok, PARSE_ERROR, UNSUPPORTED
+  int16_t kind = 0, version = 0;
+  int type = 0;  // 0 nil request, 1 typed (client + topics), 2 ConsumerMetadata
+  std::string client;
+  std::vector<std::string> topics;
+};
+
+KReq parse_kafka(const uint8_t* arena, size_t arena_bytes, uint64_t off) {
+  KReq q;
+  q.status = L7M_VERDICT_PARSE_ERROR;
+  if (off + 4 > arena_bytes) return q;
+  const uint8_t* r = arena + off;
+  int32_t msize = (int32_t)((uint32_t)r[0] << 24 | (uint32_t)r[1] << 16 | (uint32_t)r[2] << 8 | r[3]);
+  if (msize <= 0) return q;                         // io.ErrUnexpectedEOF
+  if (msize < 2) return q;                          // kind: short read
+  if ((int64_t)msize + 4 > kMaxParseBuf) return q;  // allocParseBuf
+  if (off + 4 + (uint64_t)msize > arena_bytes) return q;
+  size_t blen = 4 + (size_t)msize;
+  if (blen < 12) return q;  // "unexpected end of request"
+  q.kind = (int16_t)((r[4] << 8) | r[5]);
+  q.version = (int16_t)((r[6] << 8) | r[7]);
+  Reader rd{r, blen, 0};
+  Dec d{&rd};
+  d.i32();
+  d.i16();
+  int16_t ver = d.i16();
+  d.i32();
+  int k = q.kind;
+  if (k != 0 && k != 1 && k != 2 && k != 3 && k != 8 && k != 9 && k != 10) {
+    q.type = 0;
+    q.status = 0;
+    return q;
+  }
+  q.client = d.str();
+  q.type = (k == 10) ? 2 : 1;
+  int64_t n;
+  auto topic_list = [&](auto&& per_topic) -> bool {
+    if (!d.arraylen(&n)) return false;
+    for (int64_t t = 0; t < n; ++t) {
+      q.topics.push_back(d.str());
+      if (!per_topic()) return false;
+      if (d.err) {  // remaining iterations are no-ops; the final Err() check fails
+        return true;
+      }
+    }
+    return true;
+  };
+  bool ok = true;
+  MsRc ms = MS_OK;
+  switch (k) {
+    case 0:  // Produce
+      if (ver >= 3) d.str();
+      d.i16();
+      d.i32();
+      ok = topic_list([&]() {
+        int64_t np;
+        if (!d.arraylen(&np)) return false;
+        for (int64_t p = 0; p < np; ++p) {
+          d.i32();
+          if (d.err) return false;
+          int32_t mss = d.i32();
+          if (d.err) return false;
+          MsRc rc = read_message_set(&rd, mss, ver);
+          if (rc == MS_ERR) return false;
+          if (rc == MS_UNSUPPORTED) { ms = MS_UNSUPPORTED; return false; }
+        }
+        return true;
+      });
+      break;
+    case 1:  // Fetch
+      d.i32();
+      d.i32();
+      d.i32();
+      if (ver >= 3) d.i32();
+      if (ver >= 4) d.i8();
+      ok = topic_list([&]() {
+        int64_t np;
+        if (!d.arraylen(&np)) return false;
+        for (int64_t p = 0; p < np && !d.err; ++p) {
+          d.i32();
+          d.i64();
+          if (ver >= 5) d.i64();
+          d.i32();
+        }
+        return true;
+      });
+      break;
+    case 2:  // Offset
+      d.i32();
+      if (ver >= 2) d.i8();
+      ok = topic_list([&]() {
+        int64_t np;
+        if (!d.arraylen(&np)) return false;
+        for (int64_t p = 0; p < np && !d.err; ++p) {
+          d.i32();
+          d.i64();
+          if (ver == 0) d.i32();
+        }
+        return true;
+      });
+      break;
+    case 3:  // Metadata
+      ok = topic_list([&]() { return true; });
+      if (ok && ver >= 4) d.i8();
+      break;
+    case 8:  // OffsetCommit
+      d.str();
+      if (ver >= 1) { d.i32(); d.str(); }
+      if (ver >= 2) d.i64();
+      ok = topic_list([&]() {
+        int64_t np;
+        if (!d.arraylen(&np)) return false;
+        for (int64_t p = 0; p < np && !d.err; ++p) {
+          d.i32();
+          d.i64();
+          if (ver == 1) d.i64();
+          d.str();
+        }
+        return true;
+      });
+      break;
+    case 9:  // OffsetFetch
+      d.str();
+      ok = topic_list([&]() {
+        int64_t np;
+        if (!d.arraylen(&np)) return false;
+        for (int64_t p = 0; p < np && !d.err; ++p) d.i32();
+        return true;
+      });
+      break;
+    case 10:  // ConsumerMetadata
+      d.str();
+      if (ver >= 1) d.i8();
+      break;
+  }
+  if (ms == MS_UNSUPPORTED) { q.status = L7M_VERDICT_UNSUPPORTED; return q; }
+  if (!ok || d.err) { q.status = L7M_VERDICT_PARSE_ERROR; return q; }
+  if (k == 10) q.topics.clear();  // GetTopics: nil for ConsumerMetadata
+  q.status = 0;
+  return q;
+}
+
+bool is_topic_api_key(int16_t k) {
+  switch (k) {
+    case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 8: case 9: case 19: case 20:
+    case 21: case 23: case 24: case 27: case 28: case 34: case 35: case 37:
+      return true;
+  }
+  return false;
+}
+
+bool rule_matches(const KReq& q, const KRule& r) {
+  if (!r.keys.empty()) {
+    bool hit = false;
+    for (int16_t k : r.keys) hit |= k == q.kind;
+    if (!hit) return false;
+  }
+  if (r.has_version && r.version != q.version) return false;
+  if (r.topic.empty() && r.client.empty()) return true;
+  if (q.type == 1) return r.client.empty() || r.client == q.client;
+  if (q.type == 2) return true;
+  return !(!r.topic.empty() && is_topic_api_key(q.kind));
+}
+
+int32_t eval_kafka_one(const KafkaOracle& o, const KReq& q) {
+  if (q.status) return q.status;
+  std::set<std::string> left(q.topics.begin(), q.topics.end());
+  for (size_t i = 0; i < o.rules.size(); ++i) {
+    const KRule& r = o.rules[i];
+    if (r.topic.empty() || q.topics.empty()) {
+      if (rule_matches(q, r)) return (int32_t)i;
+    } else if (left.count(r.topic)) {
+      if (rule_matches(q, r)) {
+        left.erase(r.topic);
+        if (left.empty()) return (int32_t)i;
+      }
+    }
+  }
+  return L7M_VERDICT_DENY;
+}
+
+template <class F>
+void parallel_for(size_t n, int threads, F&& f) {
+  if (threads <= 1 || n < 1024) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t)
+    th.emplace_back([&, t]() {
+      size_t a = n * t / threads, b = n * (t + 1) / threads;
+      for (size_t i = a; i < b; ++i) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int orc_http_new(const l7m_http_rule* rules, size_t n, void** out, char* err, size_t errlen) {
+  auto* o = new HttpOracle();
+  for (size_t i = 0; i < n; ++i) {
+    const l7m_http_rule& r = rules[i];
+    std::vector<Matcher> ms;
+    if (!S(r.path).empty()) ms.push_back({":path", S(r.path), true});
+    if (!S(r.method).empty()) ms.push_back({":method", S(r.method), true});
+    if (!S(r.host).empty()) ms.push_back({":authority", S(r.host), true});
+    for (uint32_t j = 0; j < r.n_headers; ++j) {
+      std::string h = S(r.headers[j]);
+      size_t sp = h.find(' ');
+      if (sp != std::string::npos) {
+        std::string k = h.substr(0, sp);
+        while (!k.empty() && k.back() == ':') k.pop_back();
+        ms.push_back({k, h.substr(sp + 1), false});
+      } else {
+        ms.push_back({h, "", false});
+      }
+    }
+    for (size_t a = 0; a < ms.size(); ++a)
+      for (size_t b = a + 1; b < ms.size(); ++b)
+        if (ms[a].name == ms[b].name && ms[a].value == ms[b].value && !(ms[a].has_regex && ms[b].has_regex)) {
+          set_err(err, errlen, "sort panic: duplicate header matcher");
+          delete o;
+          return L7M_EINVAL_RULE;
+        }
+    std::sort(ms.begin(), ms.end(), hm_less);
+    std::vector<HeaderData> hds;
+    for (auto& m : ms) {
+      if (m.name.empty()) {
+        set_err(err, errlen, "empty header name");
+        delete o;
+        return L7M_EINVAL_RULE;
+      }
+      HeaderData hd;
+      hd.lname = m.name;
+      for (auto& c : hd.lname) c = (char)tolower((unsigned char)c);
+      hd.value = m.value;
+      if (m.value.empty()) hd.kind = 2;
+      else if (m.has_regex) {
+        hd.kind = 0;
+        try {
+          hd.re = std::regex(m.value, std::regex::optimize);
+        } catch (const std::regex_error& e) {
+          set_err(err, errlen, std::string("regex: ") + e.what());
+          delete o;
+          return L7M_EINVAL_REGEX;
+        }
+      } else hd.kind = 1;
+      hds.push_back(std::move(hd));
+    }
+    o->rules.push_back(std::move(hds));
+    std::unordered_set<uint32_t> rem;
+    for (uint32_t j = 0; j < r.n_remote_ids; ++j) rem.insert(r.remote_ids[j]);
+    o->remotes.push_back(std::move(rem));
+  }
+  *out = o;
+  return L7M_OK;
+}
+
+int orc_http_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint64_t* offs, size_t n,
+                  int32_t* verdicts, int threads) {
+  const HttpOracle& o = *static_cast<HttpOracle*>(h);
+  parallel_for(n, threads, [&](size_t i) { verdicts[i] = eval_http_one(o, parse_http(arena, arena_bytes, offs[i])); });
+  return L7M_OK;
+}
+
+void orc_http_free(void* h) { delete static_cast<HttpOracle*>(h); }
+
+int orc_regex_match(const char* pattern, const char* input, size_t input_len) {
+  try {
+    std::regex re(pattern, std::regex::optimize);
+    return std::regex_match(std::string(input, input_len), re) ? 1 : 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+int orc_kafka_new(const l7m_kafka_rule* rules, size_t n, void** out, char* err, size_t errlen) {
+  auto* o = new KafkaOracle();
+  for (size_t i = 0; i < n; ++i) {
+    KRule r;
+    std::string e;
+    int rc = sanitize(rules[i], &r, &e);
+    if (rc) {
+      set_err(err, errlen, "rule " + std::to_string(i) + ": " + e);
+      delete o;
+      return rc;
+    }
+    o->rules.push_back(std::move(r));
+  }
+  *out = o;
+  return L7M_OK;
+}
+
+int orc_kafka_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint64_t* offs, size_t n,
+                   int32_t* verdicts, int threads) {
+  const KafkaOracle& o = *static_cast<KafkaOracle*>(h);
+  parallel_for(n, threads, [&](size_t i) { verdicts[i] = eval_kafka_one(o, parse_kafka(arena, arena_bytes, offs[i])); });
+  return L7M_OK;
+}
+
+void orc_kafka_free(void* h) { delete static_cast<KafkaOracle*>(h); }
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// Differential fuzzer: libl7match's ECMAScript parser + DFA builder versus
+// libstdc++ std::regex_match (the engine Envoy applies to HeaderMatcher
+// regexes, envoy/cilium_network_policy.h:68-71).  Test infrastructure only.
+//   fuzz_regex <seed> <n_patterns> <strings_per_pattern>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <regex>
+#include <string>
+#include <vector>
+
+#include "../../cilium_amd/csrc/regex_ecma.h"
+
+using namespace l7m::re;
+static std::mt19937_64 rng;
+static int rnd(int n) { return (int)(rng() % (uint64_t)n); }
+
+static const char* kAtoms[] = {"a", "b", "c", "x", ".", "\\d", "\\w", "\\s", "\\D", "\\W", "\\S",
+  "[ab]", "[^a]", "[a-c]", "[]", "[^]", "[\\d-]", "[-a]", "[a-]", "\\.", "/", "-", "_", "0", "9",
+  "[[:alpha:]]", "[[:digit:]x]", "[^[:space:]]", "\\x41", "\\u0062", "\\cA", "\\k", "\\/", "[\\]a]",
+  "[[=a=]]", "[[.b.]]", "\\t", "[\\x80-\\xff]", "[A-z]", "[\\W\\d]", "\\0", "}", "]", "A", "Z"};
+
+// Nested quantifiers are rationed: libstdc++'s backtracking executor is
+// exponential on them (the reference's own catastrophic case).
+static std::string gen(int depth, bool* quant) {
+  int k = rnd(depth > 3 ? 3 : 10);
+  std::string s;
+  bool q1 = false, q2 = false, q3 = false;
+  if (k < 4) s = kAtoms[rnd(sizeof(kAtoms) / sizeof(*kAtoms))];
+  else if (k < 6) s = gen(depth + 1, &q1) + gen(depth + 1, &q2);
+  else if (k < 7) s = gen(depth + 1, &q1) + "|" + gen(depth + 1, &q2);
+  else if (k < 8) s = "(" + gen(depth + 1, &q1) + ")";
+  else if (k < 9) s = "(?:" + gen(depth + 1, &q1) + ")";
+  else s = gen(depth + 1, &q1) + gen(depth + 1, &q2) + gen(depth + 1, &q3);
+  *quant = q1 || q2 || q3;
+  int q = *quant ? rnd(10) : rnd(12);  // stacked forms only on quantifier-free bodies
+  static const char* qs[] = {"*", "+", "?", "{2}", "{0,2}", "{1,}", "*?", "+?", "??", "{0}", "**", "{1}{2}"};
+  if (rnd(3) == 0 && (!*quant || rnd(40) == 0)) {
+    s = "(?:" + s + ")" + qs[q];
+    *quant = true;
+  }
+  if (rnd(20) == 0) s = "^" + s;
+  if (rnd(20) == 0) s = s + "$";
+  return s;
+}
+
+static std::string rand_input() {
+  static const char alpha[] = "abcxABZ09_ -./\t\n\r]}";
+  int n = rnd(8);
+  std::string s;
+  for (int i = 0; i < n; ++i) {
+    if (rnd(16) == 0) s.push_back((char)rnd(256));
+    else s.push_back(alpha[rnd(sizeof(alpha) - 1)]);
+  }
+  return s;
+}
+
+static bool dfa_match(const Dfa& d, const std::string& s, uint32_t pat) {
+  uint32_t st = d.start;
+  for (unsigned char c : s) st = d.next[st * d.ncls + d.cmap[c]];
+  const auto& set = d.sets[d.endset[st]];
+  for (uint32_t p : set) if (p == pat) return true;
+  return false;
+}
+
+int main(int argc, char** argv) {
+  rng.seed(argc > 1 ? strtoull(argv[1], 0, 10) : 1);
+  int npat = argc > 2 ? atoi(argv[2]) : 2000;
+  int nstr = argc > 3 ? atoi(argv[3]) : 200;
+  long checked = 0, mism = 0, unsup = 0, rejected = 0, parse_mism = 0;
+  for (int i = 0; i < npat; ++i) {
+    bool qq = false;
+    std::string p = gen(0, &qq);
+    if (getenv("FUZZ_TRACE")) { fprintf(stderr, "P %d %s\n", i, p.c_str()); }
+    std::regex r;
+    bool ok = true;
+    try { r = std::regex(p, std::regex::ECMAScript | std::regex::optimize); } catch (...) { ok = false; }
+    Ast a; std::string err;
+    Status st = parse_ecma(p, &a, &err);
+    if (!ok) { rejected++; continue; }
+    if (st == Status::Unsupported) { unsup++; continue; }
+    if (st != Status::Ok) { parse_mism++; printf("PARSE-MISMATCH %s : %s\n", p.c_str(), err.c_str()); continue; }
+    // Two-pattern DFA (pattern + a literal) also exercises multi-pattern sets.
+    Ast lit = literal_ast("ab");
+    Dfa d; DfaLimits lim;
+    if (build_dfa({&a, &lit}, lim, &d) != Status::Ok) { printf("BUILD-FAIL %s\n", p.c_str()); continue; }
+    std::vector<std::string> ins;
+    for (int j = 0; j < nstr; ++j) ins.push_back(rand_input());
+    ins.push_back(""); ins.push_back("ab");
+    for (const auto& s : ins) {
+      bool ref = std::regex_match(s, r);
+      bool got = dfa_match(d, s, 0);
+      bool gotlit = dfa_match(d, s, 1);
+      checked++;
+      if (ref != got || gotlit != (s == "ab")) {
+        mism++;
+        if (mism < 30) {
+          printf("MISMATCH pat=%s in=", p.c_str());
+          for (unsigned char c : s) printf("\\x%02x", c);
+          printf(" ref=%d got=%d\n", ref, got);
+        }
+      }
+    }
+  }
+  printf("checked=%ld mismatches=%ld unsupported=%ld rejected_by_std=%ld parse_mismatch=%ld\n",
+         checked, mism, unsup, rejected, parse_mism);
+  return (mism || parse_mism) ? 1 : 0;
+}

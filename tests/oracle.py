@@ -1,0 +1,91 @@
+"""ctypes binding of the CPU oracle (oracle/liboracle.so).  TEST INFRASTRUCTURE
+ONLY: used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+as the checker, never by the product path."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from cilium_amd import l7match as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+
+
+def _load():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    lib = ctypes.CDLL(ORACLE_SO)
+    P, sz = ctypes.c_void_p, ctypes.c_size_t
+    lib.orc_http_new.argtypes = [ctypes.POINTER(L._HttpRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.orc_http_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
+    lib.orc_http_free.argtypes = [P]
+    lib.orc_kafka_new.argtypes = [ctypes.POINTER(L._KafkaRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.orc_kafka_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
+    lib.orc_kafka_free.argtypes = [P]
+    lib.orc_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
+    return lib
+
+
+_lib = _load()
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"oracle error {code}: {msg}")
+        self.code = code
+
+
+class HttpOracle:
+    def __init__(self, rules):
+        keep = []
+        arr = (L._HttpRule * max(1, len(rules)))(*[L._http_rule_struct(r, keep) for r in rules])
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.orc_http_new(arr, len(rules), ctypes.byref(h), err, 512)
+        if rc != 0:
+            raise OracleError(rc, err.value.decode(errors="replace"))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.orc_http_free(self._h)
+
+    def eval(self, arena, offsets, threads=1):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        v = np.empty(offsets.shape[0], dtype=np.int32)
+        _lib.orc_http_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
+                           offsets.shape[0], v.ctypes.data, threads)
+        return v
+
+
+class KafkaOracle:
+    def __init__(self, rules):
+        arr = (L._KafkaRule * max(1, len(rules)))(*[
+            L._KafkaRule(L._b(r.Role) or None, L._b(r.APIKey) or None, L._b(r.APIVersion) or None,
+                         L._b(r.ClientID) or None, L._b(r.Topic) or None) for r in rules])
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.orc_kafka_new(arr, len(rules), ctypes.byref(h), err, 512)
+        if rc != 0:
+            raise OracleError(rc, err.value.decode(errors="replace"))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.orc_kafka_free(self._h)
+
+    def eval(self, arena, offsets, threads=1):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        v = np.empty(offsets.shape[0], dtype=np.int32)
+        _lib.orc_kafka_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
+                            offsets.shape[0], v.ctypes.data, threads)
+        return v
+
+
+def regex_match(pattern: str, value: bytes) -> int:
+    """std::regex_match(value, std::regex(pattern, optimize)) -> 1/0, -1 if invalid."""
+    return _lib.orc_regex_match(pattern.encode(), value, len(value))
