@@ -64,6 +64,10 @@ def cpu_baseline(cfg, rules, seconds, threads):
                       f"oracle/l7oracle.cc (std::regex_match linear rule scan) on {threads} threads"}
 
 
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -82,6 +86,7 @@ def main():
     rs = L.RuleSet.compile_http(rules) if c["proto"] == L.PROTO_HTTP else L.RuleSet.compile_kafka(rules)
 
     # ---- rank's shard, generated deterministically, resident in HBM --------
+    log(f"rank {rank}: compiled {len(rules)} rules; generating {per_gpu} requests")
     t0 = time.perf_counter()
     arena, offs = W.requests(cfg, rank * per_gpu, per_gpu, threads=threads)
     gen_s = time.perf_counter() - t0
@@ -107,6 +112,7 @@ def main():
         if world > 1:
             dist.all_reduce(d_hits)
 
+    log(f"rank {rank}: arena {arena_nbytes / 1e9:.2f} GB resident (gen {gen_s:.1f} s, h2d {h2d_s:.2f} s); warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -168,7 +174,9 @@ def main():
             "counters_ok": hits_total == expect_hits,
             "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
         }
+        log(f"timed {args.steps} steps: {elapsed:.3f} s; kernel {kavg * 1e3:.2f} ms")
         if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds, threads)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -8,6 +8,15 @@
 #pragma once
 #include <stdint.h>
 
+// Host-only translation units see the HIP attributes as no-ops (HIP sources
+// include hip_runtime.h before this header).
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
+
 namespace l7m {
 
 constexpr uint32_t kMagicHttp = 0x5048374cu;   // "L7HP"
@@ -86,35 +95,59 @@ static_assert(sizeof(HttpHeader) == 128, "header is 32 words");
 // Rule semantics follow pkg/kafka/policy.go:144-225 and
 // pkg/policy/api/kafka.go:248-271 (after Sanitize, rule_validation.go:190-233).
 struct KafkaRuleDesc {
-  uint32_t keys_lo, keys_hi;  // apiKeyInt as a bitmask over kinds 0..63
-  uint32_t flags;             // bit0: apiKeyInt empty (any kind); bit1: version set;
-                              // bit2: topic set; bit3: clientID set
-  int32_t version;            // apiVersionInt when set
-  uint32_t client_off, client_len;  // bytes in the string area
-  uint32_t topic_off, topic_len;
+  uint32_t flags;        // kKRule* bits
+  int32_t version;       // apiVersionInt when kKRuleVersion
+  uint32_t keys_lo;      // apiKeyInt as a bitmask over kinds 0..63 (unless kKRuleAnyKey)
+  uint32_t keys_hi;
+  uint32_t client_hash;  // fnv1a32(ClientID) when kKRuleClient
+  uint32_t client_off;   // byte offset of ClientID in the string area
+  uint32_t client_len;
+  uint32_t pad;
 };
 constexpr uint32_t kKRuleAnyKey = 1u, kKRuleVersion = 2u, kKRuleTopic = 4u, kKRuleClient = 8u;
 
-// Open-addressed topic table: hash -> Span of rule ids (sorted) whose Topic
-// equals that string.
+// Open-addressed (linear probing) table: Topic -> ascending ids of the rules
+// whose Topic equals it.  hash == 0 marks an empty slot (see kafka_key_hash).
 struct KafkaTopicSlot {
-  uint32_t hash;      // FNV-1a 32 of the topic; 0 marks an empty slot (hash 0 remapped)
-  uint32_t str_off, str_len;
-  uint32_t list_off, list_len;
+  uint32_t hash;
+  uint32_t str_off, str_len;  // bytes in the string area
+  Span rules;                 // into the u32 pool
   uint32_t pad[3];
 };
+
+constexpr uint32_t kKafkaKinds = 65;  // request kinds 0..63; [64] = any other value
 
 struct KafkaHeader {
   uint32_t magic;
   uint32_t n_rules;
-  uint32_t off_rules;       // KafkaRuleDesc[n_rules]
-  uint32_t off_strings;     // byte area (word offset)
-  uint32_t off_pool;        // u32 pool
-  uint32_t off_slots;       // KafkaTopicSlot[n_slots]
-  uint32_t n_slots;         // power of two (0 when no topic rules)
-  Span notopic_by_kind[65]; // rules with Topic=="" allowing kind k (k<64), [64] = other kinds
-  Span all_by_kind[65];     // every rule allowing kind k (used when the request has no topics)
+  uint32_t off_rules;    // KafkaRuleDesc[n_rules]
+  uint32_t off_slots;    // KafkaTopicSlot[n_slots]
+  uint32_t n_slots;      // power of two (0 when no rule has a Topic)
+  uint32_t off_pool;     // u32 pool
+  uint32_t off_crc;      // u32[256] CRC-32 (IEEE) table for message-set CRCs
+  uint32_t off_strings;  // byte area (word offset)
   uint32_t total_words;
+  uint32_t pad[7];
+  // Ascending ids of the rules whose CheckAPIKeyRole(kind) holds:
+  Span notopic_by_kind[kKafkaKinds];  // ... and Topic == ""
+  Span all_by_kind[kKafkaKinds];      // ... any Topic
 };
+static_assert(sizeof(KafkaRuleDesc) == 32, "rule desc is 8 words");
+static_assert(sizeof(KafkaTopicSlot) == 32, "slot is 8 words");
+
+constexpr uint32_t kFnvBasis = 2166136261u;
+__host__ __device__ inline uint32_t fnv1a_step(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }
+// Table key: FNV-1a 32 with 0 remapped (0 marks an empty slot).
+__host__ __device__ inline uint32_t kafka_key_hash(uint32_t h) { return h ? h : 1u; }
+
+// isTopicAPIKey (pkg/kafka/policy.go:27-52) as a mask over kinds 0..63.
+constexpr uint64_t kTopicApiKeyMask =
+    (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3) | (1ull << 4) | (1ull << 5) |
+    (1ull << 6) | (1ull << 8) | (1ull << 9) | (1ull << 19) | (1ull << 20) | (1ull << 21) |
+    (1ull << 23) | (1ull << 24) | (1ull << 27) | (1ull << 28) | (1ull << 34) | (1ull << 35) |
+    (1ull << 37);
+
+// optiopay/kafka maxParseBufSize (vendor/github.com/optiopay/kafka/proto/utils.go:9).
+constexpr int64_t kKafkaMaxParseBuf = 100LL * 65535;
 
 }  // namespace l7m
