@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 from cilium_amd import l7match as L  # noqa: E402
 from cilium_amd import workloads as W  # noqa: E402
 
+METRIC = "L7 verdicts/sec (HTTP reqs, 1k rules) + achieved HBM GB/s vs peak"  # BASELINE.json
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -90,8 +91,7 @@ def main():
     t0 = time.perf_counter()
     arena, offs = W.requests(cfg, rank * per_gpu, per_gpu, threads=threads)
     gen_s = time.perf_counter() - t0
-    rec_bytes = int(offs[-1]) + int(np.frombuffer(arena[int(offs[-1]):int(offs[-1]) + 4].tobytes(), np.uint32)[0])
-    rec_bytes = (rec_bytes + 3) & ~3
+    rec_bytes = arena.nbytes - 64  # W.requests: packed (4-byte padded) records + 64 B tail pad
     pinned = torch.from_numpy(arena).pin_memory()
     d_arena = torch.empty(arena.nbytes, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -151,7 +151,7 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": "L7 verdicts/sec (HTTP reqs, 1k rules) + achieved HBM GB/s vs peak",
+            "metric": METRIC if cfg == 2 else f"L7 verdicts/sec ({c['name']}) + achieved HBM GB/s vs peak",
             "value": value,
             "unit": "verdicts/s",
             "n_gpus": world,

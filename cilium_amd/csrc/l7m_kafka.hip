@@ -1,7 +1,470 @@
+// l7m_kafka.hip — CDNA4 (gfx950) kernel of the batched Kafka verdict path.
+//
+// One lane per request record (the raw size-prefixed wire request as
+// proto.ReadReq returns it).  Each lane
+//   1. decodes the request exactly as kafka.ReadRequest does
+//      (pkg/kafka/request.go:186-229 -> vendor/github.com/optiopay/kafka/proto
+//      messages.go per-kind readers, decoder error semantics of
+//      serialization.go:31-196), including message-set walking with CRC-32
+//      checks (messages.go:357-483, CRC table staged in LDS);
+//   2. streams every topic name through the Topic -> rules hash table while it
+//      is decoded (no per-request topic storage), and
+//   3. resolves (*RequestMessage).MatchesRule (pkg/kafka/policy.go:200-225):
+//        no topics             -> first rule i with ruleMatches
+//        topics T (non-empty)  -> min(first Topic=="" rule with ruleMatches,
+//                                     max over t in T of first rule with
+//                                     Topic==t and ruleMatches)
+//      which is the index at which the reference's ordered loop returns true
+//      (the max term is the rule that removes the last uncovered topic).
+// Verdicts: -1 deny, -2 ReadRequest error, -3 compressed message set, i >= 0
+// allowed by rule i.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/l7match.h"
 #include "l7m_device.h"
+#include "program.h"
+
 namespace l7m {
-hipError_t launch_kafka(const uint32_t*, const KafkaHeader&, const uint8_t*, uint64_t, const uint64_t*,
-                        uint64_t, int32_t*, unsigned long long*, hipStream_t, int) {
-  return hipErrorInvalidValue;
+namespace {
+
+// A view of a byte range with the optiopay decoder's sticky-error semantics:
+// a short read consumes what is left (io.ReadFull) and sets err.
+struct Rd {
+  const uint8_t* p;
+  uint32_t len;
+  uint32_t pos;
+  bool err;
+};
+
+__device__ __forceinline__ uint64_t rd_be(Rd& d, uint32_t n) {
+  if (d.err) return 0;
+  if (d.len - d.pos < n) {
+    d.pos = d.len;
+    d.err = true;
+    return 0;
+  }
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < n; ++i) v = (v << 8) | d.p[d.pos + i];
+  d.pos += n;
+  return v;
 }
+__device__ __forceinline__ int8_t rd_i8(Rd& d) { return static_cast<int8_t>(rd_be(d, 1)); }
+__device__ __forceinline__ int16_t rd_i16(Rd& d) { return static_cast<int16_t>(rd_be(d, 2)); }
+__device__ __forceinline__ int32_t rd_i32(Rd& d) { return static_cast<int32_t>(rd_be(d, 4)); }
+
+// DecodeString (serialization.go:120-153): *off/*len of the bytes, len 0 = "".
+__device__ __forceinline__ void rd_str(Rd& d, uint32_t* off, uint32_t* len) {
+  *off = 0;
+  *len = 0;
+  if (d.err) return;
+  const int16_t n = rd_i16(d);
+  if (d.err || n < 1) return;
+  if (d.len - d.pos < static_cast<uint32_t>(n)) {
+    d.pos = d.len;
+    d.err = true;
+    return;
+  }
+  *off = d.pos;
+  *len = static_cast<uint32_t>(n);
+  d.pos += static_cast<uint32_t>(n);
+}
+
+// DecodeArrayLen (serialization.go:155-163): false = ErrInvalidArrayLen.
+__device__ __forceinline__ bool rd_arraylen(Rd& d, int32_t* n) {
+  const int32_t v = rd_i32(d);
+  if (v < 0 || v > kKafkaMaxParseBuf) return false;
+  *n = v;
+  return true;
+}
+
+// DecodeBytes (serialization.go:165-192), value discarded.
+__device__ __forceinline__ void rd_skip_bytes(Rd& d) {
+  if (d.err) return;
+  const int32_t n = rd_i32(d);
+  if (d.err || n < 1) return;
+  if (n > kKafkaMaxParseBuf) {  // allocParseBuf
+    d.err = true;
+    return;
+  }
+  if (d.len - d.pos < static_cast<uint32_t>(n)) {
+    d.pos = d.len;
+    d.err = true;
+    return;
+  }
+  d.pos += static_cast<uint32_t>(n);
+}
+
+enum { kMsOk = 0, kMsErr = 1, kMsUnsupported = 2 };
+
+// readMessageSet (messages.go:357-483) over the next `size` bytes of d.
+__device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint32_t* crc_tab) {
+  if (size < 0 || size > kKafkaMaxParseBuf) return kMsErr;
+  const uint32_t avail = d.len - d.pos;
+  Rd r{d.p + d.pos, avail < static_cast<uint32_t>(size) ? avail : static_cast<uint32_t>(size), 0, false};
+  int rc = kMsOk;
+  for (;;) {
+    rd_be(r, 8);  // offset
+    if (r.err) break;
+    const int32_t msz = rd_i32(r);
+    if (r.err || msz <= 0) break;
+    if (msz > kKafkaMaxParseBuf) {
+      rc = kMsErr;
+      break;
+    }
+    if (r.len - r.pos < static_cast<uint32_t>(msz)) {  // truncated last message
+      r.pos = r.len;
+      break;
+    }
+    const uint8_t* mb = r.p + r.pos;
+    r.pos += static_cast<uint32_t>(msz);
+    Rd m{mb, static_cast<uint32_t>(msz), 0, false};
+    const uint32_t crc = static_cast<uint32_t>(rd_be(m, 4));
+    if (msz <= 4) break;
+    uint32_t c = 0xffffffffu;
+    for (uint32_t i = 4; i < static_cast<uint32_t>(msz); ++i) c = crc_tab[(c ^ mb[i]) & 0xffu] ^ (c >> 8);
+    if (crc != (c ^ 0xffffffffu)) break;  // ignore the rest of the set
+    rd_i8(m);                              // magic
+    const int8_t attr = rd_i8(m);
+    if (version >= 1) rd_be(m, 8);         // timestamp
+    const int comp = attr & 3;
+    if (comp == 3) break;                  // `return nil, err` with err == nil
+    rd_skip_bytes(m);                      // key
+    rd_skip_bytes(m);                      // value
+    if (m.err) {
+      rc = kMsErr;
+      break;
+    }
+    if (comp != 0) {  // gzip / snappy: nested set not decompressed here
+      rc = kMsUnsupported;
+      break;
+    }
+  }
+  d.pos += r.pos;
+  return rc;
+}
+
+struct KView {
+  const uint32_t* prog;
+  const KafkaRuleDesc* rules;
+  const KafkaTopicSlot* slots;
+  const uint32_t* pool;
+  const uint8_t* strings;
+  uint32_t n_slots;
+};
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// ruleMatches (policy.go:144-195) minus CheckAPIKeyRole, which list
+// membership already guarantees: version, then the ClientID condition when
+// `check_client` (typed requests with a Topic/ClientID-bearing rule).
+__device__ __forceinline__ bool rule_rest_ok(const KView& v, uint32_t rid, int16_t version, bool check_client,
+                                             const uint8_t* client, uint32_t client_len, uint32_t client_hash) {
+  const KafkaRuleDesc r = v.rules[rid];
+  if ((r.flags & kKRuleVersion) && r.version != version) return false;
+  if (check_client && (r.flags & kKRuleClient)) {
+    if (r.client_len != client_len || r.client_hash != client_hash) return false;
+    if (!bytes_eq(v.strings + r.client_off, client, client_len)) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool key_ok(const KafkaRuleDesc& r, int32_t kind) {
+  if (r.flags & kKRuleAnyKey) return true;
+  if (kind < 0 || kind >= 64) return false;
+  return kind < 32 ? ((r.keys_lo >> kind) & 1u) : ((r.keys_hi >> (kind - 32)) & 1u);
+}
+
+// First rule of an ascending candidate list (ids < limit) passing rule_rest_ok.
+__device__ uint32_t first_in(const KView& v, Span s, uint32_t limit, int16_t version, bool check_client,
+                             const uint8_t* client, uint32_t client_len, uint32_t client_hash) {
+  for (uint32_t j = 0; j < s.len; ++j) {
+    const uint32_t rid = v.pool[s.off + j];
+    if (rid >= limit) break;
+    if (rule_rest_ok(v, rid, version, check_client, client, client_len, client_hash)) return rid;
+  }
+  return kNone;
+}
+
+// Per-request coverage state of the topic walk (policy.go:210-223).
+struct Cover {
+  uint32_t j;      // first Topic=="" rule with ruleMatches (kNone if none)
+  uint32_t maxf;   // max over topics of the first covering rule
+  bool ok;         // every topic so far has a covering rule below j
+};
+
+__device__ void cover_topic(const KView& v, Cover& cv, const uint8_t* t, uint32_t tlen, int32_t kind,
+                            int16_t version, const uint8_t* client, uint32_t client_len,
+                            uint32_t client_hash) {
+  if (!cv.ok) return;
+  uint32_t f = kNone;
+  if (tlen && v.n_slots) {
+    uint32_t h = kFnvBasis;
+    for (uint32_t i = 0; i < tlen; ++i) h = fnv1a_step(h, t[i]);
+    h = kafka_key_hash(h);
+    for (uint32_t at = h & (v.n_slots - 1);; at = (at + 1) & (v.n_slots - 1)) {
+      const KafkaTopicSlot sl = v.slots[at];
+      if (sl.hash == 0) break;
+      if (sl.hash == h && sl.str_len == tlen && bytes_eq(v.strings + sl.str_off, t, tlen)) {
+        for (uint32_t j = 0; j < sl.rules.len; ++j) {
+          const uint32_t rid = v.pool[sl.rules.off + j];
+          if (rid >= cv.j) break;
+          if (key_ok(v.rules[rid], kind) &&
+              rule_rest_ok(v, rid, version, true, client, client_len, client_hash)) {
+            f = rid;
+            break;
+          }
+        }
+        break;
+      }
+    }
+  }
+  // A topic without a covering rule below j leaves min(j, .) = j.
+  if (f == kNone) cv.ok = false;
+  else if (f > cv.maxf || cv.maxf == kNone) cv.maxf = f;
+}
+
+__device__ int32_t eval_kafka(const KView& v, const KafkaHeader& h, const uint8_t* __restrict__ arena,
+                              uint64_t arena_bytes, uint64_t off, const uint32_t* crc_tab) {
+  if ((off & 3) || off + 4 > arena_bytes) return L7M_VERDICT_PARSE_ERROR;
+  const uint8_t* rec = arena + off;
+  const int32_t msize = static_cast<int32_t>((static_cast<uint32_t>(rec[0]) << 24) |
+                                             (static_cast<uint32_t>(rec[1]) << 16) |
+                                             (static_cast<uint32_t>(rec[2]) << 8) | rec[3]);
+  // ReadReq: size <= 0 / short kind read / allocParseBuf; ReadRequest: len < 12.
+  if (msize < 8 || static_cast<int64_t>(msize) + 4 > kKafkaMaxParseBuf) return L7M_VERDICT_PARSE_ERROR;
+  if (off + 4 + static_cast<uint64_t>(msize) > arena_bytes) return L7M_VERDICT_PARSE_ERROR;
+  const int32_t kind = static_cast<int16_t>((rec[4] << 8) | rec[5]);
+  const int16_t version = static_cast<int16_t>((rec[6] << 8) | rec[7]);  // request.go:72-74
+  const uint32_t kidx = (kind >= 0 && kind < 64) ? static_cast<uint32_t>(kind) : 64u;
+
+  uint32_t first = kNone;
+  const bool typed = kind == 0 || kind == 1 || kind == 2 || kind == 3 || kind == 8 || kind == 9 || kind == 10;
+  if (!typed) {
+    // request == nil: matchNonTopicRequests (policy.go:54-70), ClientID ignored.
+    const bool topic_kind = kind >= 0 && kind < 64 && ((kTopicApiKeyMask >> kind) & 1ull);
+    first = first_in(v, topic_kind ? h.notopic_by_kind[kidx] : h.all_by_kind[kidx], kNone, version, false,
+                     nullptr, 0, 0);
+  } else {
+    Rd d{rec, 4u + static_cast<uint32_t>(msize), 12, false};
+    uint32_t coff, clen;
+    rd_str(d, &coff, &clen);
+    const uint8_t* client = rec + coff;
+    uint32_t chash = kFnvBasis;
+    for (uint32_t i = 0; i < clen; ++i) chash = fnv1a_step(chash, client[i]);
+
+    int32_t ntop = 0;
+    bool ok = true;
+    int ms = kMsOk;
+    Cover cv{kNone, kNone, true};
+    // Called after the topic array length is known: j (the Topic=="" rules)
+    // is needed only when there are topics.
+    auto start_topics = [&](int32_t n) {
+      ntop = n;
+      if (n > 0 && kind != 10) {
+        cv.j = first_in(v, h.notopic_by_kind[kidx], kNone, version, true, client, clen, chash);
+      }
+    };
+    auto topic = [&]() {
+      uint32_t toff, tlen;
+      rd_str(d, &toff, &tlen);
+      if (!d.err) cover_topic(v, cv, rec + toff, tlen, kind, version, client, clen, chash);
+    };
+    int32_t n, np;
+    switch (kind) {
+      case 0: {  // ReadProduceReq messages.go:1572-1628
+        if (version >= 3) {
+          uint32_t a, b;
+          rd_str(d, &a, &b);
+        }
+        rd_i16(d);
+        rd_i32(d);
+        if (!rd_arraylen(d, &n)) { ok = false; break; }
+        start_topics(n);
+        for (int32_t t = 0; t < n && ok && ms == kMsOk; ++t) {
+          topic();
+          if (!rd_arraylen(d, &np)) { ok = false; break; }
+          for (int32_t p = 0; p < np; ++p) {
+            rd_i32(d);
+            if (d.err) { ok = false; break; }
+            const int32_t mss = rd_i32(d);
+            if (d.err) { ok = false; break; }
+            const int rc = read_message_set(d, mss, version, crc_tab);
+            if (rc == kMsErr) { ok = false; break; }
+            if (rc == kMsUnsupported) { ms = rc; break; }
+          }
+          if (d.err) break;  // remaining iterations are no-ops; Err() fails below
+        }
+        break;
+      }
+      case 1: {  // ReadFetchReq messages.go:752-809
+        rd_i32(d);
+        rd_i32(d);
+        rd_i32(d);
+        if (version >= 3) rd_i32(d);
+        if (version >= 4) rd_i8(d);
+        if (!rd_arraylen(d, &n)) { ok = false; break; }
+        start_topics(n);
+        for (int32_t t = 0; t < n && ok; ++t) {
+          topic();
+          if (!rd_arraylen(d, &np)) { ok = false; break; }
+          for (int32_t p = 0; p < np && !d.err; ++p) {
+            rd_i32(d);
+            rd_be(d, 8);
+            if (version >= 5) rd_be(d, 8);
+            rd_i32(d);
+          }
+          if (d.err) break;
+        }
+        break;
+      }
+      case 2: {  // ReadOffsetReq messages.go:1791-1839
+        rd_i32(d);
+        if (version >= 2) rd_i8(d);
+        if (!rd_arraylen(d, &n)) { ok = false; break; }
+        start_topics(n);
+        for (int32_t t = 0; t < n && ok; ++t) {
+          topic();
+          if (!rd_arraylen(d, &np)) { ok = false; break; }
+          for (int32_t p = 0; p < np && !d.err; ++p) {
+            rd_i32(d);
+            rd_be(d, 8);
+            if (version == 0) rd_i32(d);
+          }
+          if (d.err) break;
+        }
+        break;
+      }
+      case 3: {  // ReadMetadataReq messages.go:493-522
+        if (!rd_arraylen(d, &n)) { ok = false; break; }
+        start_topics(n);
+        for (int32_t t = 0; t < n; ++t) {
+          topic();
+          if (d.err) break;
+        }
+        if (version >= 4) rd_i8(d);
+        break;
+      }
+      case 8: {  // ReadOffsetCommitReq messages.go:1158-1213
+        uint32_t a, b;
+        rd_str(d, &a, &b);
+        if (version >= 1) {
+          rd_i32(d);
+          rd_str(d, &a, &b);
+        }
+        if (version >= 2) rd_be(d, 8);
+        if (!rd_arraylen(d, &n)) { ok = false; break; }
+        start_topics(n);
+        for (int32_t t = 0; t < n && ok; ++t) {
+          topic();
+          if (!rd_arraylen(d, &np)) { ok = false; break; }
+          for (int32_t p = 0; p < np && !d.err; ++p) {
+            rd_i32(d);
+            rd_be(d, 8);
+            if (version == 1) rd_be(d, 8);
+            rd_str(d, &a, &b);
+          }
+          if (d.err) break;
+        }
+        break;
+      }
+      case 9: {  // ReadOffsetFetchReq messages.go:1374-1411
+        uint32_t a, b;
+        rd_str(d, &a, &b);
+        if (!rd_arraylen(d, &n)) { ok = false; break; }
+        start_topics(n);
+        for (int32_t t = 0; t < n && ok; ++t) {
+          topic();
+          if (!rd_arraylen(d, &np)) { ok = false; break; }
+          for (int32_t p = 0; p < np && !d.err; ++p) rd_i32(d);
+          if (d.err) break;
+        }
+        break;
+      }
+      default: {  // 10: ReadConsumerMetadataReq messages.go:1018-1039
+        uint32_t a, b;
+        rd_str(d, &a, &b);
+        if (version >= 1) rd_i8(d);
+        break;
+      }
+    }
+    if (ms == kMsUnsupported) return L7M_VERDICT_UNSUPPORTED;
+    if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
+    if (kind == 10) {
+      // ConsumerMetadataReq: GetTopics() is nil and ruleMatches -> true.
+      first = first_in(v, h.all_by_kind[kidx], kNone, version, false, nullptr, 0, 0);
+    } else if (ntop == 0) {
+      first = first_in(v, h.all_by_kind[kidx], kNone, version, true, client, clen, chash);
+    } else {
+      first = cv.ok ? cv.maxf : cv.j;
+      if (cv.j < first) first = cv.j;
+    }
+  }
+  return first == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(first);
+}
+
+__device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits, uint32_t slot, bool active) {
+  uint64_t todo = __ballot(active);
+  const uint32_t lane = __lane_id();
+  while (todo) {
+    const uint32_t leader = __builtin_ctzll(todo);
+    const uint32_t key = __shfl(slot, leader);
+    const uint64_t same = __ballot(active && slot == key) & todo;
+    if (lane == leader) atomicAdd(hits + key, static_cast<unsigned long long>(__popcll(same)));
+    todo &= ~same;
+  }
+}
+
+template <bool kHits>
+__global__ __launch_bounds__(256) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
+                                                         const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                         const uint64_t* __restrict__ offs, uint64_t n,
+                                                         int32_t* __restrict__ verdicts,
+                                                         unsigned long long* __restrict__ hits) {
+  __shared__ uint32_t crc_tab[256];
+  const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) crc_tab[i] = prog[h.off_crc + i];
+  __syncthreads();
+  KView v;
+  v.prog = prog;
+  v.rules = reinterpret_cast<const KafkaRuleDesc*>(prog + h.off_rules);
+  v.slots = reinterpret_cast<const KafkaTopicSlot*>(prog + h.off_slots);
+  v.pool = prog + h.off_pool;
+  v.strings = reinterpret_cast<const uint8_t*>(prog + h.off_strings);
+  v.n_slots = h.n_slots;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; r < n; r += stride) {
+    const int32_t verdict = eval_kafka(v, h, arena, arena_bytes, offs[r], crc_tab);
+    verdicts[r] = verdict;
+    if (kHits) {
+      const uint32_t slot = verdict >= 0 ? static_cast<uint32_t>(verdict) + 2 : (verdict == -1 ? 0u : 1u);
+      count_slot(hits, slot, true);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
+                        const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
+                        hipStream_t stream, int num_cus) {
+  (void)h;
+  if (n == 0) return hipSuccess;
+  const uint32_t block = 256;
+  uint64_t blocks = (n + block - 1) / block;
+  const uint64_t cap = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * 8;
+  if (blocks > cap) blocks = cap;
+  if (hits)
+    hipLaunchKernelGGL(kafka_eval_kernel<true>, dim3(static_cast<uint32_t>(blocks)), dim3(block), 0, stream, dprog,
+                       arena, arena_bytes, offs, n, verdicts, hits);
+  else
+    hipLaunchKernelGGL(kafka_eval_kernel<false>, dim3(static_cast<uint32_t>(blocks)), dim3(block), 0, stream, dprog,
+                       arena, arena_bytes, offs, n, verdicts, hits);
+  return hipGetLastError();
+}
+
 }  // namespace l7m

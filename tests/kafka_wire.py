@@ -1,0 +1,186 @@
+"""Kafka request encoder for tests (TEST INFRASTRUCTURE).
+
+Writes requests in the wire layout the reference's decoder reads: the
+per-kind readers of vendor/github.com/optiopay/kafka/proto/messages.go
+(ReadProduceReq :1572-1628, ReadFetchReq :752-809, ReadOffsetReq :1791-1839,
+ReadMetadataReq :493-522, ReadOffsetCommitReq :1158-1213, ReadOffsetFetchReq
+:1374-1411, ReadConsumerMetadataReq :1018-1039) and readMessageSet
+(:357-483; message CRC as writeMessageSet :271-300 computes it).  A record is
+the size-prefixed request exactly as proto.ReadReq returns it.
+"""
+import struct
+import zlib
+
+PRODUCE, FETCH, OFFSETS, METADATA, OFFSET_COMMIT, OFFSET_FETCH, CONSUMER_METADATA = 0, 1, 2, 3, 8, 9, 10
+
+
+def s(x):
+    """Kafka STRING (int16 length; None = null, length -1)."""
+    if x is None:
+        return struct.pack(">h", -1)
+    b = x.encode() if isinstance(x, str) else bytes(x)
+    return struct.pack(">h", len(b)) + b
+
+
+def b(x):
+    """Kafka BYTES (int32 length; None = null, length -1)."""
+    if x is None:
+        return struct.pack(">i", -1)
+    x = x.encode() if isinstance(x, str) else bytes(x)
+    return struct.pack(">i", len(x)) + x
+
+
+def message_set(values, version=0, compression=0, bad_crc_at=None, key=None, first_offset=0):
+    out = b""
+    for i, v in enumerate(values):
+        body = struct.pack(">bb", 0, compression)
+        if version >= 1:
+            body += struct.pack(">q", 1_500_000_000_000 + i)
+        body += b(key) + b(v)
+        crc = zlib.crc32(body) & 0xFFFFFFFF
+        if bad_crc_at == i:
+            crc ^= 1
+        m = struct.pack(">I", crc) + body
+        out += struct.pack(">qi", first_offset + i, len(m)) + m
+    return out
+
+
+def request(kind, version, client, body=b"", correlation=1):
+    payload = struct.pack(">hhi", kind, version, correlation) + s(client) + body
+    return struct.pack(">i", len(payload)) + payload
+
+
+def produce(version, client, topics, txn=None, acks=-1, timeout=1000):
+    """topics: [(name, [(partition, message_set_bytes), ...]), ...]"""
+    body = (s(txn) if version >= 3 else b"") + struct.pack(">hi", acks, timeout)
+    body += struct.pack(">i", len(topics))
+    for name, parts in topics:
+        body += s(name) + struct.pack(">i", len(parts))
+        for pid, ms in parts:
+            body += struct.pack(">ii", pid, len(ms)) + ms
+    return request(PRODUCE, version, client, body)
+
+
+def fetch(version, client, topics):
+    """topics: [(name, [partition, ...]), ...]"""
+    body = struct.pack(">iii", -1, 500, 1)
+    if version >= 3:
+        body += struct.pack(">i", 1 << 20)
+    if version >= 4:
+        body += b"\x00"
+    body += struct.pack(">i", len(topics))
+    for name, parts in topics:
+        body += s(name) + struct.pack(">i", len(parts))
+        for pid in parts:
+            body += struct.pack(">iq", pid, 42)
+            if version >= 5:
+                body += struct.pack(">q", 0)
+            body += struct.pack(">i", 1 << 20)
+    return request(FETCH, version, client, body)
+
+
+def offsets(version, client, topics):
+    body = struct.pack(">i", -1) + (b"\x00" if version >= 2 else b"")
+    body += struct.pack(">i", len(topics))
+    for name, parts in topics:
+        body += s(name) + struct.pack(">i", len(parts))
+        for pid in parts:
+            body += struct.pack(">iq", pid, -1) + (struct.pack(">i", 1) if version == 0 else b"")
+    return request(OFFSETS, version, client, body)
+
+
+def metadata(version, client, topics):
+    """topics: list of names (None = null array, which the decoder rejects)."""
+    body = struct.pack(">i", -1 if topics is None else len(topics))
+    for name in topics or []:
+        body += s(name)
+    if version >= 4:
+        body += b"\x01"
+    return request(METADATA, version, client, body)
+
+
+def offset_commit(version, client, group, topics):
+    body = s(group)
+    if version >= 1:
+        body += struct.pack(">i", 7) + s("member-1")
+    if version >= 2:
+        body += struct.pack(">q", 60_000)
+    body += struct.pack(">i", len(topics))
+    for name, parts in topics:
+        body += s(name) + struct.pack(">i", len(parts))
+        for pid in parts:
+            body += struct.pack(">iq", pid, 100)
+            if version == 1:
+                body += struct.pack(">q", 1_500_000_000_000)
+            body += s("meta")
+    return request(OFFSET_COMMIT, version, client, body)
+
+
+def offset_fetch(version, client, group, topics):
+    body = s(group) + struct.pack(">i", len(topics))
+    for name, parts in topics:
+        body += s(name) + struct.pack(">i", len(parts))
+        for pid in parts:
+            body += struct.pack(">i", pid)
+    return request(OFFSET_FETCH, version, client, body)
+
+
+def consumer_metadata(version, client, group):
+    return request(CONSUMER_METADATA, version, client, s(group) + (b"\x00" if version >= 1 else b""))
+
+
+def generic(kind, version, client="", body=b"\x00" * 8):
+    """A request of a kind ReadRequest does not decode (request == nil)."""
+    return request(kind, version, client, body)
+
+
+def random_requests(rng, n, topics, clients):
+    """Well-formed requests of every decoded kind and a few undecoded ones."""
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(0, 9))
+        cl = None if rng.random() < 0.05 else str(rng.choice(clients))
+        nt = int(rng.integers(0, 4))
+        ts = [str(rng.choice(topics)) for _ in range(nt)]
+        if k == 0:
+            v = int(rng.integers(0, 4))
+            parts = [(name, [(0, message_set(["x" * int(rng.integers(0, 20))], version=v)
+                              if rng.random() < 0.3 else b"")]) for name in ts]
+            out.append(produce(v, cl, parts, txn=None if rng.random() < 0.5 else "tx"))
+        elif k == 1:
+            out.append(fetch(int(rng.integers(0, 6)), cl, [(t, [0, 1]) for t in ts]))
+        elif k == 2:
+            out.append(offsets(int(rng.integers(0, 3)), cl, [(t, [0]) for t in ts]))
+        elif k == 3:
+            out.append(metadata(int(rng.integers(0, 5)), cl, ts))
+        elif k == 4:
+            out.append(offset_commit(int(rng.integers(0, 3)), cl, "grp", [(t, [1]) for t in ts]))
+        elif k == 5:
+            out.append(offset_fetch(int(rng.integers(0, 2)), cl, "grp", [(t, [1, 2]) for t in ts]))
+        elif k == 6:
+            out.append(consumer_metadata(int(rng.integers(0, 2)), cl, "grp"))
+        else:
+            out.append(generic(int(rng.choice([4, 11, 12, 18, 19, 36, 70, -3])), int(rng.integers(0, 3)), cl or ""))
+    return out
+
+
+def mutate(rng, rec: bytes) -> bytes:
+    """One random corruption of a record (truncation, size field, byte flips)."""
+    r = bytearray(rec)
+    k = int(rng.integers(0, 5))
+    if k == 0 and len(r) > 13:  # truncate body, keep the size field honest
+        cut = int(rng.integers(12, len(r)))
+        r = r[:cut]
+        r[0:4] = struct.pack(">i", len(r) - 4)
+    elif k == 1:  # lie about the size
+        r[0:4] = struct.pack(">i", int(rng.integers(-4, len(r) + 8)))
+    elif k == 2 and len(r) > 12:  # flip a byte after the header
+        i = int(rng.integers(12, len(r)))
+        r[i] ^= int(rng.integers(1, 256))
+    elif k == 3 and len(r) > 14:  # huge/negative length in a length field position
+        i = int(rng.integers(12, len(r) - 2))
+        r[i:i + 2] = struct.pack(">h", int(rng.choice([-1, -2, 0x7FFF, 0])))
+    else:  # append garbage (ignored trailing bytes)
+        r += bytes(rng.integers(0, 256, size=int(rng.integers(1, 9)), dtype="uint8"))
+        r[0:4] = struct.pack(">i", len(r) - 4)
+    return bytes(r)

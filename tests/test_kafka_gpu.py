@@ -1,0 +1,126 @@
+"""GPU parity tests of the Kafka path: the HIP kernel (decode + MatchesRule,
+through the C ABI) versus the CPU oracle, bit-exact int32 verdicts."""
+import numpy as np
+import pytest
+
+import kafka_wire as K
+from cilium_amd import l7match as L
+from cilium_amd import workloads as W
+from kafka_cases import LOREM, cases
+from oracle import KafkaOracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(rules, arena, offs, hits=False):
+    rs = L.RuleSet.compile_kafka(rules)
+    h = np.zeros(rs.n_counters, dtype=np.uint64) if hits else None
+    got = rs.eval(arena, offs, h)
+    exp = KafkaOracle(rules).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+    if hits:
+        assert int(h[0]) == int((exp == -1).sum())
+        assert int(h[1]) == int((exp <= -2).sum())
+        for r in np.unique(exp[exp >= 0])[:50]:
+            assert int(h[2 + r]) == int((exp == r).sum())
+        assert int(h.sum()) == len(exp)
+    return got
+
+
+@pytest.mark.parametrize("name,rules,records,expected", cases(), ids=[c[0] for c in cases()])
+def test_reference_known_answers(gpu, name, rules, records, expected):
+    arena, offs = L.pack_records(records)
+    assert _check(rules, arena, offs).tolist() == expected
+
+
+def test_config3_sample_parity(gpu):
+    rules = W.rules(3)
+    arena, offs = W.requests(3, 7_000_000, 200_000)
+    v = _check(rules, arena, offs, hits=True)
+    assert (v >= 0).any() and (v == -1).any()
+
+
+def _random_rules(rng, n, topics, clients):
+    keys = ["", "", "produce", "fetch", "metadata", "offsets", "offsetcommit", "offsetfetch",
+            "findcoordinator", "apiversions", "heartbeat"]
+    out = []
+    for _ in range(n):
+        role = str(rng.choice(["produce", "consume"])) if rng.random() < 0.2 else ""
+        out.append(L.PortRuleKafka(
+            Role=role, APIKey="" if role else str(rng.choice(keys)),
+            APIVersion=str(int(rng.integers(0, 4))) if rng.random() < 0.3 else "",
+            ClientID=str(rng.choice(clients)) if rng.random() < 0.3 else "",
+            Topic=str(rng.choice(topics)) if rng.random() < 0.7 else ""))
+    return out
+
+
+def test_random_rules_and_requests_parity(gpu):
+    rng = np.random.default_rng(5)
+    topics = ["t%d" % i for i in range(12)]
+    clients = ["c%d" % i for i in range(4)]
+    for trial in range(12):
+        rules = _random_rules(rng, int(rng.integers(1, 40)), topics, clients)
+        recs = K.random_requests(rng, 4000, topics + ["zz"], clients + ["cX"])
+        arena, offs = L.pack_records(recs)
+        _check(rules, arena, offs, hits=trial == 0)
+
+
+def test_malformed_records_parity(gpu):
+    rng = np.random.default_rng(9)
+    topics = ["t%d" % i for i in range(6)]
+    rules = _random_rules(rng, 25, topics, ["c0", "c1"]) + [L.PortRuleKafka()]
+    base = K.random_requests(rng, 6000, topics, ["c0", "c1"])
+    recs = [K.mutate(rng, r) for r in base]
+    arena, offs = L.pack_records(recs)
+    v = _check(rules, arena, offs, hits=True)
+    assert (v == L.VERDICT_PARSE_ERROR).any() and (v >= 0).any()
+
+
+def test_message_sets_crc_and_compression(gpu):
+    rules = [L.PortRuleKafka(APIKey="produce", Topic="t"), L.PortRuleKafka(Topic="u")]
+    recs = []
+    for v in range(4):
+        recs += [K.produce(v, "c", [("t", [(0, K.message_set([LOREM] * 3, version=v))])]),
+                 K.produce(v, "c", [("t", [(0, K.message_set(["a", "b"], version=v, bad_crc_at=1))]),
+                                    ("u", [(1, K.message_set(["c"], version=v))])]),
+                 K.produce(v, "c", [("t", [(0, K.message_set(["g"], version=v, compression=2))])]),
+                 K.produce(v, "c", [("t", [(0, K.message_set(["g"], version=v, compression=3))])]),
+                 K.produce(v, "c", [("t", [(0, K.message_set(["abc", "def"], version=v)[:-2])])]),
+                 K.produce(v, "c", [("t", [(0, K.message_set(["k"], version=v, key="kk"))]),
+                                    ("u", [(0, b""), (1, b"")])])]
+    arena, offs = L.pack_records(recs)
+    v = _check(rules, arena, offs)
+    assert (v == L.VERDICT_UNSUPPORTED).any()
+
+
+def test_empty_batch_empty_rules_and_bounds(gpu):
+    rs = L.RuleSet.compile_kafka([L.PortRuleKafka()])
+    assert rs.eval(np.zeros(64, np.uint8), np.zeros(0, np.uint64)).shape == (0,)
+    recs = [K.metadata(0, "c", ["a"]), K.metadata(1, "c", [])]
+    arena, offs = L.pack_records(recs)
+    assert L.RuleSet.compile_kafka([]).eval(arena, offs).tolist() == [-1, -1]
+    offs2 = offs.copy()
+    offs2[0] = arena.nbytes + 64     # outside the arena
+    offs2[1] = offs2[1] + 1          # misaligned
+    assert rs.eval(arena, offs2).tolist() == [L.VERDICT_PARSE_ERROR] * 2
+
+
+def test_eval_device_and_shard_invariance(gpu):
+    import torch
+    rules = W.rules(3)
+    rs = L.RuleSet.compile_kafka(rules)
+    arena, offs = W.requests(3, 0, 200_000)
+    host_v = rs.eval(arena, offs)
+    dev = torch.device("cuda:0")
+    da = torch.from_numpy(arena).to(dev)
+    do = torch.from_numpy(offs.view(np.int64)).to(dev)
+    dv = torch.empty(len(offs), dtype=torch.int32, device=dev)
+    dh = torch.zeros(rs.n_counters, dtype=torch.int64, device=dev)
+    rs.eval_device(da, arena.nbytes, do, len(offs), dv, dh, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert (dv.cpu().numpy() == host_v).all()
+    assert int(dh.sum()) == len(offs)
+    a1, o1 = W.requests(3, 0, 100_000)
+    a2, o2 = W.requests(3, 100_000, 100_000)
+    assert (np.concatenate([rs.eval(a1, o1), rs.eval(a2, o2)]) == host_v).all()
