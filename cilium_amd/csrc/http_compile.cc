@@ -26,6 +26,7 @@
 #include <regex>
 #include <unordered_map>
 
+#include "dfa_pack.h"
 #include "l7m_internal.h"
 #include "program.h"
 #include "regex_ecma.h"
@@ -68,7 +69,7 @@ struct FieldPattern {
 
 struct Group {
   std::vector<uint32_t> pats;  // field pattern indices (local id = position)
-  re::Dfa dfa;
+  PackedDfa pk;
 };
 
 int build_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> idx,
@@ -76,7 +77,9 @@ int build_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> 
   std::vector<const re::Ast*> sub;
   for (uint32_t i : idx) sub.push_back(asts[i]);
   Group g;
-  re::Status st = re::build_dfa(sub, lim, &g.dfa);
+  re::Dfa dfa;
+  re::Status st = re::build_dfa(sub, lim, &dfa);
+  if (st == re::Status::Ok) st = pack_dfa(dfa, &g.pk);  // TooBig: > 32K packed bases
   if (st == re::Status::Ok) {
     g.pats = std::move(idx);
     out->push_back(std::move(g));
@@ -255,7 +258,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
 
   // header-name DFA over every regular field name (exact, lower-case)
   bool has_name = nf > 3;
-  re::Dfa name_dfa;
+  PackedDfa name_dfa;
   if (has_name) {
     std::vector<re::Ast> asts;
     for (uint32_t f = 3; f < nf; ++f) asts.push_back(re::literal_ast(field_names[f]));
@@ -264,7 +267,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     re::DfaLimits nl;
     nl.max_states = 1u << 22;
     nl.max_table_bytes = 1ull << 30;
-    if (re::build_dfa(ptrs, nl, &name_dfa) != re::Status::Ok)
+    re::Dfa nd;
+    if (re::build_dfa(ptrs, nl, &nd) != re::Status::Ok || pack_dfa(nd, &name_dfa) != re::Status::Ok)
       return fail(L7M_ETOOBIG, "header-name DFA too large");
   }
 
@@ -346,31 +350,33 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   };
 
   struct DfaOut {
-    const re::Dfa* d;
+    const PackedDfa* d;
     uint32_t field;
+    uint32_t npats;
   };
   std::vector<DfaOut> all;
   for (uint32_t f = 0; f < nf; ++f)
-    for (auto& g : groups[f]) all.push_back({&g.dfa, f});
-  if (has_name) all.push_back({&name_dfa, kNone});
+    for (auto& g : groups[f]) all.push_back({&g.pk, f, static_cast<uint32_t>(g.pats.size())});
+  if (has_name) all.push_back({&name_dfa, kNone, nf - 3});
   const uint32_t ndt = static_cast<uint32_t>(all.size());
 
   std::vector<DfaDesc> dd(ndt);
-  std::vector<Span> sets, cands;
-  uint64_t table_words = 0, total_states = 0;
+  std::vector<Span> sets, cands, pcands;
+  uint64_t total_states = 0;
   for (uint32_t k = 0; k < ndt; ++k) {
-    const re::Dfa& d = *all[k].d;
-    dd[k].ncols = static_cast<uint32_t>(d.ncls) + 1;
-    dd[k].start = static_cast<uint32_t>(d.start) * dd[k].ncols;
+    const PackedDfa& d = *all[k].d;
+    std::memset(&dd[k], 0, sizeof(DfaDesc));
+    dd[k].start_desc = d.start_desc;
+    dd[k].region = d.region;
+    dd[k].start_latch = d.start_latch;
+    dd[k].n_slots = d.n_slots;
     dd[k].set_base = static_cast<uint32_t>(sets.size());
     dd[k].nsets = static_cast<uint32_t>(d.sets.size());
+    dd[k].pcand_base = static_cast<uint32_t>(pcands.size());
+    dd[k].npats = all[k].npats;
     dd[k].field = all[k].field;
-    dd[k].nstates = static_cast<uint32_t>(d.nstates);
-    dd[k].cmap_index = k;
-    dd[k].table_off = static_cast<uint32_t>(table_words);  // relative for now
-    uint64_t words = static_cast<uint64_t>(d.nstates) * dd[k].ncols;
-    if (words >= (1ull << 32)) return fail(L7M_ETOOBIG, "DFA table offset overflow");
-    table_words += words;
+    dd[k].nstates = d.nstates;
+    dd[k].lds_off = kNone;
     total_states += d.nstates;
     for (size_t s = 0; s < d.sets.size(); ++s) {
       sets.push_back(push_list(d.sets[s]));
@@ -387,6 +393,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
         cands.push_back(Span{0, 0});
       }
     }
+    for (uint32_t p = 0; p < all[k].npats; ++p)
+      pcands.push_back(k < ndfa ? push_list(keyed[k][p]) : Span{0, 0});
   }
   std::vector<uint32_t> name_field;
   if (has_name) {
@@ -415,6 +423,31 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     }
   }
 
+  // LDS image: slot tables, hottest first (header names, path, authority,
+  // method, then header values), while they fit the budget.  The rest are
+  // walked from HBM (L2 / MALL resident).
+  const uint64_t lds_budget_words = (opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget) / 4;
+  auto hotness = [&](uint32_t k) -> int {
+    const uint32_t f = all[k].field;
+    if (f == kNone) return 0;
+    if (f == kFieldPath) return 1;
+    if (f == kFieldAuthority) return 2;
+    if (f == kFieldMethod) return 3;
+    return 4;
+  };
+  std::vector<uint32_t> order(ndt);
+  for (uint32_t k = 0; k < ndt; ++k) order[k] = k;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hotness(a) < hotness(b); });
+  std::vector<uint32_t> lds_words_of(ndt, kNone);
+  uint64_t lds_words = 0;
+  for (uint32_t k : order) {
+    const uint64_t w = (all[k].d->n_slots + 3) & ~uint64_t(3);
+    if (lds_words + w <= lds_budget_words) {
+      lds_words_of[k] = static_cast<uint32_t>(lds_words);
+      lds_words += w;
+    }
+  }
+
   // layout
   HttpHeader h;
   std::memset(&h, 0, sizeof h);
@@ -436,31 +469,39 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   h.off_name_field = take(name_field.size());
   h.off_sets = take(sets.size() * 2);
   h.off_cands = take(cands.size() * 2);
+  h.off_pcands = take(pcands.size() * 2);
   h.off_rules = take(static_cast<uint64_t>(n) * 2);
   h.off_matchers = take(md.size() * 4);
   h.off_remotes = take(static_cast<uint64_t>(n) * 2);
   h.any_remotes = any_remotes ? 1u : 0u;
   h.zero_list = zero_span;
   h.off_pool = take(pool.size());
-  w = (w + 63) & ~uint64_t(63);  // 256-byte align tables
-  h.off_tables = take(table_words);
-  h.table_words = static_cast<uint32_t>(table_words);
-  h.off_cmaps = take(static_cast<uint64_t>(ndt) * 64);
+  w = (w + 63) & ~uint64_t(63);  // 256-byte align the table area
+  h.lds_image_off = take(lds_words);
+  h.lds_image_words = static_cast<uint32_t>(lds_words);
+  for (uint32_t k = 0; k < ndt; ++k) {
+    if (lds_words_of[k] != kNone) {
+      dd[k].lds_off = lds_words_of[k];
+      dd[k].table_off = h.lds_image_off + lds_words_of[k];
+    } else {
+      w = (w + 3) & ~uint64_t(3);
+      dd[k].table_off = take(all[k].d->n_slots);
+    }
+  }
+  for (uint32_t k = 0; k < ndt; ++k) {
+    dd[k].es_off = take(all[k].d->n_slots);
+    dd[k].latch_off = take(all[k].d->n_slots);
+  }
   if (w >= (1ull << 32)) return fail(L7M_ETOOBIG, "program exceeds 16 GiB");
   h.total_words = static_cast<uint32_t>(w);
 
   std::vector<uint32_t> prog(w, 0);
   std::memcpy(prog.data(), &h, sizeof h);
   for (uint32_t k = 0; k < ndt; ++k) {
-    dd[k].table_off += h.off_tables;
-    const re::Dfa& d = *all[k].d;
-    uint32_t nc = dd[k].ncols;
-    uint32_t* t = prog.data() + dd[k].table_off;
-    for (int s = 0; s < d.nstates; ++s) {
-      for (int c = 0; c < d.ncls; ++c) t[static_cast<size_t>(s) * nc + c] = d.next[static_cast<size_t>(s) * d.ncls + c] * nc;
-      t[static_cast<size_t>(s) * nc + d.ncls] = d.endset[s];
-    }
-    std::memcpy(reinterpret_cast<uint8_t*>(prog.data() + h.off_cmaps) + 256 * k, d.cmap, 256);
+    const PackedDfa& d = *all[k].d;
+    std::memcpy(prog.data() + dd[k].table_off, d.table.data(), d.n_slots * 4ull);
+    std::memcpy(prog.data() + dd[k].es_off, d.es.data(), d.n_slots * 4ull);
+    std::memcpy(prog.data() + dd[k].latch_off, d.latch.data(), d.n_slots * 4ull);
   }
   std::memcpy(prog.data() + h.off_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
   std::memcpy(prog.data() + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));
@@ -468,6 +509,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     std::memcpy(prog.data() + h.off_name_field, name_field.data(), name_field.size() * 4);
   std::memcpy(prog.data() + h.off_sets, sets.data(), sets.size() * sizeof(Span));
   std::memcpy(prog.data() + h.off_cands, cands.data(), cands.size() * sizeof(Span));
+  if (!pcands.empty()) std::memcpy(prog.data() + h.off_pcands, pcands.data(), pcands.size() * sizeof(Span));
   if (n) std::memcpy(prog.data() + h.off_rules, rspan.data(), rspan.size() * sizeof(Span));
   if (n) std::memcpy(prog.data() + h.off_remotes, rremote.data(), rremote.size() * sizeof(Span));
   if (!md.empty()) std::memcpy(prog.data() + h.off_matchers, md.data(), md.size() * sizeof(MatcherDesc));

@@ -26,10 +26,12 @@ void set_err(char* err, size_t errlen, const std::string& m) {
   err[k] = '\0';
 }
 
+// Older callers may pass a shorter l7m_opts (struct_size): copy what they set.
 l7m_opts norm_opts(const l7m_opts* o) {
   l7m_opts r{};
-  if (o && o->struct_size >= sizeof(l7m_opts)) r = *o;
-  else if (o && o->struct_size == 0) r = *o;
+  if (!o) return r;
+  size_t k = o->struct_size == 0 || o->struct_size > sizeof(l7m_opts) ? sizeof(l7m_opts) : o->struct_size;
+  std::memcpy(&r, o, k);
   return r;
 }
 
@@ -259,6 +261,8 @@ int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_byt
                     void* hip_stream, uint32_t flags) {
   (void)flags;
   if (!rs || (n && (!d_arena || !d_offsets || !d_verdicts))) return L7M_EINVAL;
+  // The kernels stream records with aligned 16-byte loads.
+  if (reinterpret_cast<uintptr_t>(d_arena) & 15) return L7M_EINVAL;
   return launch(rs, d_arena, arena_bytes, d_offsets, n, d_verdicts, d_hits, static_cast<hipStream_t>(hip_stream));
 }
 

@@ -10,6 +10,8 @@
 
 namespace l7m {
 
+constexpr uint32_t kDefaultLdsBudget = 64u * 1024u;  // bytes of DFA slot tables in LDS
+
 // One getHTTPRule HeaderMatcher (pkg/envoy/server.go:261-320).
 struct HeaderMatcher {
   std::string name;   // as emitted by getHTTPRule (not lower-cased)

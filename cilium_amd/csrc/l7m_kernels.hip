@@ -1,14 +1,20 @@
-// l7m_kernels.hip — CDNA4 (gfx950) kernels of the batched L7 verdict path.
+// l7m_kernels.hip — CDNA4 (gfx950) kernel of the batched HTTP verdict path.
 //
-// HTTP: one lane per request (a wave evaluates 64 consecutive records of the
-// arena).  Per request the lane streams the record's method / path /
-// authority / header bytes through the per-field DFAs, one dependent table
-// load per byte (`s = tab[s + cmap[b]]`, premultiplied rows, byte-class map
-// staged in LDS), records the end set of every DFA in LDS, then resolves the
-// first matching rule from the precomputed candidate lists (see
-// http_compile.cc).  Reference semantics: NetworkPolicyMap::Allowed ->
-// PortNetworkPolicyRule::Matches -> HttpNetworkPolicyRule::Matches ->
-// ConfigUtility::matchHeaders (envoy/cilium_network_policy.h:68-237).
+// One lane per request; a 512-thread workgroup is resident for many tiles of
+// 512 consecutive records (grid-stride).  Per workgroup, once:
+//   * the packed DFA slot tables that fit the LDS budget (the "LDS image",
+//     dfa_pack.h) and the DFA descriptors are copied HBM -> LDS.
+// Per request (lane):
+//   * the record is streamed from HBM with 16-byte non-temporal loads (it is
+//     read exactly once; non-temporal keeps the L2 for the rule tables);
+//   * every referenced field (method / path / authority / header values whose
+//     lower-cased name the header-name DFA recognises) is walked through its
+//     DFA groups: ONE dependent 4-byte LDS read per input byte;
+//   * the end codes select precomputed candidate rule lists; the first rule
+//     (input order) whose remaining matchers hold is the verdict.
+// Reference semantics: NetworkPolicyMap::Allowed -> PortNetworkPolicyRule::
+// Matches -> HttpNetworkPolicyRule::Matches -> ConfigUtility::matchHeaders
+// (envoy/cilium_network_policy.h:68-237).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -17,52 +23,68 @@
 #include "program.h"
 
 namespace l7m {
+namespace {
 
-struct WalkDfa {
-  const uint32_t* tab;
-  const uint8_t* cmap;  // LDS
-  uint32_t start, ncls;
-};
+constexpr uint32_t kBlock = 512;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Stream `len` bytes at rec+pos through the DFA; returns the end-set id.
-__device__ __forceinline__ uint32_t walk(const WalkDfa& d, const uint8_t* __restrict__ rec,
-                                         uint32_t pos, uint32_t len) {
-  uint32_t s = d.start;
-  if (len) {
-    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(rec);
-    uint32_t wi = pos >> 2;
-    uint32_t word = __builtin_nontemporal_load(w32 + wi) >> (8 * (pos & 3));
-    uint32_t avail = 4 - (pos & 3);
-    for (uint32_t k = 0; k < len; ++k) {
-      if (avail == 0) {
-        ++wi;
-        word = __builtin_nontemporal_load(w32 + wi);
-        avail = 4;
-      }
-      uint32_t b = word & 0xffu;
-      word >>= 8;
-      --avail;
-      s = d.tab[s + d.cmap[b]];
-      if (s == 0) break;  // dead state: no pattern of this DFA can match
-    }
-  }
-  return d.tab[s + d.ncls];
+__device__ __forceinline__ uint32_t sel4(const u32x4& v, uint32_t q) {
+  uint32_t r = v.x;
+  r = q == 1u ? v.y : r;
+  r = q == 2u ? v.z : r;
+  r = q == 3u ? v.w : r;
+  return r;
 }
 
-__device__ __forceinline__ WalkDfa load_dfa(const uint32_t* __restrict__ prog, const HttpHeader& h,
-                                            const uint8_t* cmaps_lds, uint32_t k) {
-  const DfaDesc* dd = reinterpret_cast<const DfaDesc*>(prog + h.off_dfas) + k;
-  WalkDfa w;
-  w.tab = prog + dd->table_off;
-  w.cmap = cmaps_lds + 256u * dd->cmap_index;
-  w.start = dd->start;
-  w.ncls = dd->ncols - 1;
-  return w;
+// Walk `len` bytes at p through one packed DFA whose slot table is T (LDS or
+// global).  Returns the end code: 0, a set id, or kLatchedBit | pattern.
+template <bool kLds>
+__device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ T, const DfaDesc& dd,
+                                         const uint32_t* __restrict__ prog, const uint8_t* p, uint32_t len) {
+  uint32_t desc = dd.start_desc;
+  uint32_t last = kNone;
+  if (len && desc) {
+    const uint32_t region = dd.region;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const u32x4* cp = reinterpret_cast<const u32x4*>(a & ~uintptr_t(15));
+    uint32_t o = static_cast<uint32_t>(a & 15u);
+    u32x4 ch = __builtin_nontemporal_load(cp);
+    uint32_t w = sel4(ch, o >> 2) >> (8u * (o & 3u));
+    uint32_t base = desc >> 1;
+    for (uint32_t k = 0;;) {
+      const uint32_t slot = base + (w & 0xffu);
+      const uint32_t e = T[slot];
+      if (base < region) last = slot;
+      desc = ((e & 0xffffu) == base) ? (e >> 16) : ((desc & 1u) ? desc : 0u);
+      base = desc >> 1;
+      if (++k == len || desc == 0u) break;
+      ++o;
+      w >>= 8;
+      if ((o & 3u) == 0u) {
+        if (o == 16u) {
+          ++cp;
+          ch = __builtin_nontemporal_load(cp);
+          o = 0;
+        }
+        w = sel4(ch, o >> 2);
+      }
+    }
+  }
+  if (!desc) return 0;
+  const uint32_t es = prog[dd.es_off + (desc >> 1)];
+  if (es == kLatchedBit) return kLatchedBit | (last == kNone ? dd.start_latch : prog[dd.latch_off + last]);
+  return es;
+}
+
+__device__ __forceinline__ uint32_t walk_any(const uint32_t* img, const DfaDesc& dd, const uint32_t* prog,
+                                             const uint8_t* p, uint32_t len) {
+  if (dd.lds_off != kNone) return walk<true>(img + dd.lds_off, dd, prog, p, len);
+  return walk<false>(prog + dd.table_off, dd, prog, p, len);
 }
 
 __device__ __forceinline__ bool set_has(const uint32_t* __restrict__ pool, Span s, uint32_t p) {
   for (uint32_t j = 0; j < s.len; ++j) {
-    uint32_t v = pool[s.off + j];
+    const uint32_t v = pool[s.off + j];
     if (v == p) return true;
     if (v > p) return false;  // sorted
   }
@@ -70,52 +92,53 @@ __device__ __forceinline__ bool set_has(const uint32_t* __restrict__ pool, Span 
 }
 
 // Per-wave aggregated counter increment: one atomic per distinct slot.
-__device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits, uint32_t slot,
-                                           bool active) {
+__device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits, uint32_t slot, bool active) {
   uint64_t todo = __ballot(active);
   const uint32_t lane = __lane_id();
   while (todo) {
-    uint32_t leader = __builtin_ctzll(todo);
-    uint32_t key = __shfl(slot, leader);
-    uint64_t same = __ballot(active && slot == key) & todo;
+    const uint32_t leader = __builtin_ctzll(todo);
+    const uint32_t key = __shfl(slot, leader);
+    const uint64_t same = __ballot(active && slot == key) & todo;
     if (lane == leader) atomicAdd(hits + key, static_cast<unsigned long long>(__popcll(same)));
     todo &= ~same;
   }
 }
 
 template <bool kHits>
-__global__ __launch_bounds__(256) void http_eval_kernel(const uint32_t* __restrict__ prog,
-                                                        const uint8_t* __restrict__ arena,
-                                                        uint64_t arena_bytes,
-                                                        const uint64_t* __restrict__ offs,
-                                                        uint64_t n, int32_t* __restrict__ verdicts,
-                                                        unsigned long long* __restrict__ hits) {
-  extern __shared__ __align__(16) uint8_t smem[];
+__global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,
+                                                           const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                           const uint64_t* __restrict__ offs, uint64_t n,
+                                                           int32_t* __restrict__ verdicts,
+                                                           unsigned long long* __restrict__ hits) {
+  extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t ndt = h.n_dfas + h.has_name_dfa;
-  uint8_t* cmaps = smem;
-  uint32_t* sids = reinterpret_cast<uint32_t*>(smem + 256u * ndt);
+  uint32_t* img = smem;
+  DfaDesc* dds = reinterpret_cast<DfaDesc*>(smem + h.lds_image_words);
+  uint32_t* sids = smem + h.lds_image_words + 16u * ndt;
+  const uint32_t tid = threadIdx.x;
   {
-    const uint32_t* g = prog + h.off_cmaps;
-    uint32_t* l = reinterpret_cast<uint32_t*>(cmaps);
-    for (uint32_t i = threadIdx.x; i < 64u * ndt; i += blockDim.x) l[i] = g[i];
+    const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
+    uint4* l = reinterpret_cast<uint4*>(img);
+    for (uint32_t i = tid; i < h.lds_image_words / 4u; i += kBlock) l[i] = g[i];
+    const uint4* gd = reinterpret_cast<const uint4*>(prog + h.off_dfas);
+    uint4* ld = reinterpret_cast<uint4*>(dds);
+    for (uint32_t i = tid; i < 4u * ndt; i += kBlock) ld[i] = gd[i];
   }
   __syncthreads();
 
-  const uint32_t tid = threadIdx.x;
-  const uint32_t bd = blockDim.x;
   const FieldDesc* fields = reinterpret_cast<const FieldDesc*>(prog + h.off_fields);
   const Span* sets = reinterpret_cast<const Span*>(prog + h.off_sets);
   const Span* cands = reinterpret_cast<const Span*>(prog + h.off_cands);
+  const Span* pcands = reinterpret_cast<const Span*>(prog + h.off_pcands);
   const Span* rules = reinterpret_cast<const Span*>(prog + h.off_rules);
   const MatcherDesc* mds = reinterpret_cast<const MatcherDesc*>(prog + h.off_matchers);
-  const DfaDesc* dds = reinterpret_cast<const DfaDesc*>(prog + h.off_dfas);
   const uint32_t* pool = prog + h.off_pool;
   const uint32_t* name_field = prog + h.off_name_field;
   const Span* remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
 
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * bd;
-  for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * bd + tid; r < n; r += stride) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
+  for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + tid; r < n; r += stride) {
     const uint64_t off = offs[r];
     // Malformed record (outside the arena or inconsistent lengths): report
     // it instead of reading out of bounds.
@@ -151,14 +174,14 @@ __global__ __launch_bounds__(256) void http_eval_kernel(const uint32_t* __restri
       continue;
     }
     uint64_t present = 0;
-    for (uint32_t d = 0; d < h.n_dfas; ++d) sids[d * bd + tid] = 0;
+    for (uint32_t d = 0; d < h.n_dfas; ++d) sids[d * kBlock + tid] = 0;
 
     uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
     auto eval_field = [&](uint32_t f, uint32_t p, uint32_t len) {
       const FieldDesc fd = fields[f];
       for (uint32_t k = 0; k < fd.ndfa; ++k) {
-        WalkDfa wd = load_dfa(prog, h, cmaps, fd.dfa_first + k);
-        sids[(fd.dfa_first + k) * bd + tid] = walk(wd, rec, p, len);
+        const uint32_t d = fd.dfa_first + k;
+        sids[d * kBlock + tid] = walk_any(img, dds[d], prog, rec + p, len);
       }
     };
     if (flags & L7M_HTTP_F_METHOD) {
@@ -177,12 +200,14 @@ __global__ __launch_bounds__(256) void http_eval_kernel(const uint32_t* __restri
     }
     pos += alen;
     if (h.has_name_dfa) {
-      WalkDfa nd = load_dfa(prog, h, cmaps, h.n_dfas);
+      const DfaDesc& nd = dds[h.n_dfas];
       for (uint32_t j = 0; j < nhdr; ++j) {
         const uint32_t e = rw[5 + j];
         const uint32_t nl = e & 0xffffu, vl = e >> 16;
-        const uint32_t sid = walk(nd, rec, pos, nl);
-        const uint32_t f = sid ? name_field[sid] : kNone;
+        const uint32_t code = walk_any(img, nd, prog, rec + pos, nl);
+        uint32_t f = kNone;
+        if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
+        else if (code) f = name_field[code];
         if (f != kNone && !((present >> f) & 1ull)) {  // first occurrence wins
           present |= 1ull << f;
           eval_field(f, pos + nl, vl);
@@ -212,9 +237,13 @@ __global__ __launch_bounds__(256) void http_eval_kernel(const uint32_t* __restri
         const MatcherDesc m = mds[rs.off + j];
         if (!((present >> m.field) & 1ull)) return false;
         if (m.kind == 0) {
-          const uint32_t sid = sids[m.dfa * bd + tid];
-          if (sid == 0) return false;
-          if (!set_has(pool, sets[dds[m.dfa].set_base + sid], m.pattern)) return false;
+          const uint32_t code = sids[m.dfa * kBlock + tid];
+          if (code == 0) return false;
+          if (code & kLatchedBit) {
+            if ((code & ~kLatchedBit) != m.pattern) return false;
+          } else if (!set_has(pool, sets[dds[m.dfa].set_base + code], m.pattern)) {
+            return false;
+          }
         }
       }
       return true;
@@ -230,8 +259,9 @@ __global__ __launch_bounds__(256) void http_eval_kernel(const uint32_t* __restri
       }
     };
     for (uint32_t d = 0; d < h.n_dfas; ++d) {
-      const uint32_t sid = sids[d * bd + tid];
-      if (sid) scan(cands[dds[d].set_base + sid]);
+      const uint32_t code = sids[d * kBlock + tid];
+      if (code & kLatchedBit) scan(pcands[dds[d].pcand_base + (code & ~kLatchedBit)]);
+      else if (code) scan(cands[dds[d].set_base + code]);
     }
     for (uint32_t f = 0; f < h.n_fields; ++f)
       if ((present >> f) & 1ull) scan(fields[f].presence);
@@ -254,25 +284,32 @@ __global__ __launch_bounds__(256) void http_eval_kernel(const uint32_t* __restri
   }
 }
 
+}  // namespace
+
 size_t http_lds_bytes(const HttpHeader& h, uint32_t block) {
-  return 256u * (h.n_dfas + h.has_name_dfa) + static_cast<size_t>(h.n_dfas) * block * 4u;
+  (void)block;
+  const size_t ndt = h.n_dfas + h.has_name_dfa;
+  return 4u * (static_cast<size_t>(h.lds_image_words) + 16u * ndt + static_cast<size_t>(h.n_dfas) * kBlock);
 }
 
-hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena,
-                       uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                       unsigned long long* hits, hipStream_t stream, int num_cus) {
+hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena, uint64_t arena_bytes,
+                       const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
+                       hipStream_t stream, int num_cus) {
   if (n == 0) return hipSuccess;
-  const uint32_t block = 256;
-  uint64_t blocks = (n + block - 1) / block;
-  uint64_t cap = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * 8;
+  const size_t lds = http_lds_bytes(h, kBlock);
+  // Workgroups stay resident for many tiles: size the grid to what fits.
+  uint64_t per_cu = lds ? (160u * 1024u) / lds : 4;
+  if (per_cu > 4) per_cu = 4;
+  if (per_cu < 1) per_cu = 1;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * per_cu;
   if (blocks > cap) blocks = cap;
-  size_t lds = http_lds_bytes(h, block);
   if (hits)
-    hipLaunchKernelGGL(http_eval_kernel<true>, dim3(static_cast<uint32_t>(blocks)), dim3(block), lds,
-                       stream, dprog, arena, arena_bytes, offs, n, verdicts, hits);
+    hipLaunchKernelGGL(http_eval_kernel<true>, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), lds, stream, dprog,
+                       arena, arena_bytes, offs, n, verdicts, hits);
   else
-    hipLaunchKernelGGL(http_eval_kernel<false>, dim3(static_cast<uint32_t>(blocks)), dim3(block), lds,
-                       stream, dprog, arena, arena_bytes, offs, n, verdicts, hits);
+    hipLaunchKernelGGL(http_eval_kernel<false>, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), lds, stream, dprog,
+                       arena, arena_bytes, offs, n, verdicts, hits);
   return hipGetLastError();
 }
 

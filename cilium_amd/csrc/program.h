@@ -19,7 +19,7 @@
 
 namespace l7m {
 
-constexpr uint32_t kMagicHttp = 0x5048374cu;   // "L7HP"
+constexpr uint32_t kMagicHttp = 0x3248374cu;   // "L7H2" (packed DFA layout)
 constexpr uint32_t kMagicKafka = 0x504b374cu;  // "L7KP"
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kMaxFields = 64;            // present-mask is one u64 per request
@@ -34,21 +34,33 @@ struct Span {
   uint32_t off, len;  // into the u32 pool
 };
 
-// One DFA group.  Table rows are (ncls + 1) words wide; entries hold the
-// *premultiplied* row offset of the next state (state * ncols), so a step is
-// one load:  s = tab[s + cmap[byte]].  Column ncls holds the end-set id
-// (patterns matched if the value ends in this state).  Row 0 is the dead
-// state (all entries 0, end set 0 = empty).
+// One DFA group in packed double-array form (dfa_pack.h).  A walk starts at
+// start_desc and performs, per input byte b,
+//     e = T[base + b];  desc = (e & 0xffff) == base ? e >> 16 : (desc & 1 ? desc : 0)
+// over the u32 slot table T (LDS image when lds_off != kNone, else HBM/L2).
+// The walk's end code is es[base]: 0 (no pattern), a set id (index into this
+// DFA's sets/cands), or kLatchedAccept (0x80000000) meaning "the latched
+// pattern", which is latch[slot of the transition that entered the latched
+// region] (bases >= region), or start_latch.
 struct DfaDesc {
-  uint32_t table_off;   // word offset of row 0
-  uint32_t ncols;       // ncls + 1
-  uint32_t start;       // premultiplied start row
-  uint32_t set_base;    // index of this DFA's set 0 in sets[] / cands[]
+  uint32_t table_off;    // word offset of slot 0 in the program
+  uint32_t lds_off;      // word offset of slot 0 in the LDS image, or kNone
+  uint32_t start_desc;   // (base << 1) | selfdef; 0 = dead (nothing can match)
+  uint32_t region;       // bases >= region are latched (single-pattern) states
+  uint32_t start_latch;  // pattern of a latched start state, else kNone
+  uint32_t es_off;       // u32[n_slots]: end code per base
+  uint32_t latch_off;    // u32[n_slots]: latched pattern per slot
+  uint32_t n_slots;
+  uint32_t set_base;     // index of this DFA's set 0 in sets[] / cands[]
   uint32_t nsets;
-  uint32_t field;       // field this DFA evaluates (kNone for the name DFA)
+  uint32_t pcand_base;   // index of this DFA's pattern 0 in pcands[]
+  uint32_t npats;
+  uint32_t field;        // field this DFA evaluates (kNone for the name DFA)
   uint32_t nstates;
-  uint32_t cmap_index;  // 256-byte class map number
+  uint32_t pad[2];
 };
+static_assert(sizeof(DfaDesc) == 64, "dfa desc is 16 words");
+constexpr uint32_t kLatchedBit = 0x80000000u;
 
 struct FieldDesc {
   uint32_t dfa_first, ndfa;  // value DFAs of this field (contiguous)
@@ -80,9 +92,9 @@ struct HttpHeader {
   uint32_t off_rules;      // Span[n_rules] into matchers (units of MatcherDesc)
   uint32_t off_matchers;   // MatcherDesc[]
   uint32_t off_pool;       // u32 pool
-  uint32_t off_tables;     // start of all DFA tables
-  uint32_t table_words;    // words of all DFA tables
-  uint32_t off_cmaps;      // (n_dfas + has_name_dfa) * 64 words of byte->class maps
+  uint32_t off_pcands;     // Span[total patterns]: sorted rule ids keyed on the pattern
+  uint32_t lds_image_off;  // program words [off, off + words) are copied to LDS
+  uint32_t lds_image_words;
   uint32_t total_words;
   uint32_t off_remotes;    // Span[n_rules]: sorted allowed remote ids (len 0 = any)
   uint32_t any_remotes;    // 1 if no rule restricts the remote identity

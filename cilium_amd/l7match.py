@@ -76,7 +76,8 @@ class _KafkaRule(ctypes.Structure):
 class _Opts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("dialect", ctypes.c_uint32),
                 ("max_dfa_states", ctypes.c_uint32), ("flags", ctypes.c_uint32),
-                ("max_table_bytes", ctypes.c_uint64)]
+                ("max_table_bytes", ctypes.c_uint64), ("lds_budget_bytes", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class _Info(ctypes.Structure):
@@ -325,17 +326,18 @@ class RuleSet:
         return buf
 
     @staticmethod
-    def _opts(dialect: int, max_dfa_states: int, max_table_bytes: int) -> _Opts:
-        return _Opts(ctypes.sizeof(_Opts), dialect, max_dfa_states, 0, max_table_bytes)
+    def _opts(dialect: int, max_dfa_states: int, max_table_bytes: int, lds_budget_bytes: int = 0) -> _Opts:
+        return _Opts(ctypes.sizeof(_Opts), dialect, max_dfa_states, 0, max_table_bytes, lds_budget_bytes, 0)
 
     @classmethod
     def compile_http(cls, rules: Sequence[PortRuleHTTP], dialect: int = DIALECT_ENVOY_ECMA_FULL,
-                     max_dfa_states: int = 0, max_table_bytes: int = 0) -> "RuleSet":
+                     max_dfa_states: int = 0, max_table_bytes: int = 0,
+                     lds_budget_bytes: int = 0) -> "RuleSet":
         keep: list = []
         arr = (_HttpRule * max(1, len(rules)))(*[_http_rule_struct(r, keep) for r in rules])
         out = ctypes.c_void_p()
         err = ctypes.create_string_buffer(1024)
-        opts = cls._opts(dialect, max_dfa_states, max_table_bytes)
+        opts = cls._opts(dialect, max_dfa_states, max_table_bytes, lds_budget_bytes)
         rc = _lib.l7m_compile_http(arr, len(rules), ctypes.byref(opts), ctypes.byref(out), err, 1024)
         if rc != L7M_OK:
             raise L7Error(rc, err.value.decode(errors="replace"))

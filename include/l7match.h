@@ -106,6 +106,9 @@ typedef struct {
   uint32_t max_dfa_states;  /* per DFA group before splitting (0 = default)     */
   uint32_t flags;           /* reserved, 0                                      */
   uint64_t max_table_bytes; /* per DFA group before splitting (0 = default)     */
+  uint32_t lds_budget_bytes;/* DFA slot tables kept in LDS per workgroup
+                               (0 = default 64 KiB); the rest is walked from HBM */
+  uint32_t reserved;
 } l7m_opts;
 
 typedef struct {
@@ -200,7 +203,9 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
 
 /* Device-resident variant: all pointers are device pointers on the current HIP
  * device; the work is enqueued on `hip_stream` (NULL = default stream) and the
- * call returns without synchronising. */
+ * call returns without synchronising.  d_arena must be 16-byte aligned and
+ * readable up to round_up(arena_bytes, 16) (records are streamed with aligned
+ * 16-byte loads); L7M_EINVAL otherwise. */
 int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes,
                     const void* d_rec_offsets, size_t n, void* d_verdicts, void* d_rule_hits,
                     void* hip_stream, uint32_t flags);

@@ -12,25 +12,29 @@ import numpy as np
 from cilium_amd import l7match as L
 
 KNONE = 0xFFFFFFFF
+LATCHED = 0x80000000
 HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_dfa off_dfas "
               "off_fields off_name_field off_sets off_cands off_rules off_matchers off_pool "
-              "off_tables table_words off_cmaps total_words off_remotes any_remotes zero_off zero_len").split()
+              "off_pcands lds_image_off lds_image_words total_words off_remotes any_remotes "
+              "zero_off zero_len").split()
+DFA_FIELDS = ("table_off lds_off start_desc region start_latch es_off latch_off n_slots set_base nsets "
+              "pcand_base npats field nstates").split()
 
 
 class HttpProgram:
     def __init__(self, prog: np.ndarray):
         self.w = prog.astype(np.uint64).astype(np.int64).tolist()
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
-        assert self.h["magic"] == 0x5048374C
+        assert self.h["magic"] == 0x3248374C
         h = self.h
         ndt = h["n_dfas"] + h["has_name_dfa"]
         self.dfas = []
         for k in range(ndt):
-            o = h["off_dfas"] + 8 * k
-            table_off, ncols, start, set_base, nsets, fld, nstates, cmi = self.w[o:o + 8]
-            cm = prog.view(np.uint8)[4 * h["off_cmaps"] + 256 * cmi: 4 * h["off_cmaps"] + 256 * (cmi + 1)]
-            self.dfas.append(dict(table_off=table_off, ncols=ncols, start=start, set_base=set_base,
-                                  nsets=nsets, field=fld, cmap=cm.tolist()))
+            o = h["off_dfas"] + 16 * k
+            d = dict(zip(DFA_FIELDS, self.w[o:o + len(DFA_FIELDS)]))
+            if d["lds_off"] != KNONE:  # the LDS image is a copy of program words
+                assert d["table_off"] == h["lds_image_off"] + d["lds_off"]
+            self.dfas.append(d)
         self.fields = []
         for f in range(h["n_fields"]):
             o = h["off_fields"] + 4 * f
@@ -46,15 +50,30 @@ class HttpProgram:
         return self.w[b:b + n]
 
     def walk(self, k, data: bytes):
+        """Packed double-array walk (cilium_amd/csrc/dfa_pack.h): end code."""
         d = self.dfas[k]
-        tab = d["table_off"]
-        s = d["start"]
-        ncls = d["ncols"] - 1
+        T = d["table_off"]
+        desc = d["start_desc"]
+        base = desc >> 1
+        last = KNONE
         for b in data:
-            s = self.w[tab + s + d["cmap"][b]]
-            if s == 0:
+            if not desc:
                 break
-        return self.w[tab + s + ncls]
+            slot = base + b
+            e = self.w[T + slot]
+            if base < d["region"]:
+                last = slot
+            if (e & 0xFFFF) == base:
+                desc = e >> 16
+            elif not desc & 1:
+                desc = 0
+            base = desc >> 1
+        if not desc:
+            return 0
+        es = self.w[d["es_off"] + base]
+        if es == LATCHED:
+            return LATCHED | (d["start_latch"] if last == KNONE else self.w[d["latch_off"] + last])
+        return es
 
     def eval_record(self, rec: bytes) -> int:
         h = self.h
@@ -82,8 +101,11 @@ class HttpProgram:
         if h["has_name_dfa"]:
             for e in dirs:
                 nl, vl = e & 0xFFFF, e >> 16
-                sid = self.walk(h["n_dfas"], rec[pos:pos + nl])
-                f = self.w[h["off_name_field"] + sid] if sid else KNONE
+                code = self.walk(h["n_dfas"], rec[pos:pos + nl])
+                if code & LATCHED:
+                    f = 3 + (code & ~LATCHED)
+                else:
+                    f = self.w[h["off_name_field"] + code] if code else KNONE
                 if f != KNONE and not (present >> f) & 1:
                     present |= 1 << f
                     eval_field(f, rec[pos + nl:pos + nl + vl])
@@ -101,10 +123,13 @@ class HttpProgram:
                 if not (present >> fld) & 1:
                     return False
                 if kind == 0:
-                    sid = sids[dfa]
-                    if sid == 0:
+                    code = sids[dfa]
+                    if code == 0:
                         return False
-                    if pat not in self.pool(self.span(h["off_sets"], self.dfas[dfa]["set_base"] + sid)):
+                    if code & LATCHED:
+                        if code & ~LATCHED != pat:
+                            return False
+                    elif pat not in self.pool(self.span(h["off_sets"], self.dfas[dfa]["set_base"] + code)):
                         return False
             return True
 
@@ -117,8 +142,11 @@ class HttpProgram:
             return best
 
         for d in range(h["n_dfas"]):
-            if sids[d]:
-                best = scan(self.span(h["off_cands"], self.dfas[d]["set_base"] + sids[d]), best)
+            code = sids[d]
+            if code & LATCHED:
+                best = scan(self.span(h["off_pcands"], self.dfas[d]["pcand_base"] + (code & ~LATCHED)), best)
+            elif code:
+                best = scan(self.span(h["off_cands"], self.dfas[d]["set_base"] + code), best)
         for f in range(h["n_fields"]):
             if (present >> f) & 1:
                 best = scan((self.fields[f][2], self.fields[f][3]), best)
