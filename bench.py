@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--no-hits", action="store_true", help="skip the per-rule counters (diagnostic)")
+    ap.add_argument("--lds-budget", type=int, default=0, help="bytes of rule tables kept in LDS (0 = default)")
     return ap.parse_args()
 
 
@@ -84,7 +86,8 @@ def main():
     threads = args.threads or max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
 
     rules = W.rules(cfg)
-    rs = L.RuleSet.compile_http(rules) if c["proto"] == L.PROTO_HTTP else L.RuleSet.compile_kafka(rules)
+    rs = (L.RuleSet.compile_http(rules, lds_budget_bytes=args.lds_budget) if c["proto"] == L.PROTO_HTTP
+          else L.RuleSet.compile_kafka(rules))
 
     # ---- rank's shard, generated deterministically, resident in HBM --------
     log(f"rank {rank}: compiled {len(rules)} rules; generating {per_gpu} requests")
@@ -106,9 +109,11 @@ def main():
     d_hits = torch.zeros(rs.n_counters, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
 
+    hits_arg = None if args.no_hits else d_hits
+
     def step():
         d_hits.zero_()
-        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, d_hits, stream.cuda_stream)
+        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream)
         if world > 1:
             dist.all_reduce(d_hits)
 
@@ -125,7 +130,7 @@ def main():
     for i in range(args.steps):
         d_hits.zero_()
         ev[i][0].record(stream)
-        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, d_hits, stream.cuda_stream)
+        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream)
         ev[i][1].record(stream)
         if world > 1:
             dist.all_reduce(d_hits)

@@ -22,7 +22,6 @@ struct U32VecHash {
 
 struct Row {
   int orig;                   // representative original DFA state
-  bool selfdef = false;
   std::vector<uint8_t> bytes;  // explicit bytes (ascending)
   std::vector<uint32_t> tgt;   // new-state id per explicit byte
   uint32_t base = 0;
@@ -182,25 +181,17 @@ re::Status pack_dfa(const re::Dfa& d, PackedDfa* out) {
       if (blk[s] >= 0) nid[s] = bid[blk[s]];
   }
 
-  // 4. rows over raw bytes with a dead/self default.
+  // 4. rows over raw bytes: every non-dead transition is explicit.
   uint64_t n_explicit = 0;
   for (uint32_t i = 0; i < rows.size(); ++i) {
     Row& r = rows[i];
-    const uint32_t self = i + 1;
-    uint32_t tg[256];
-    int cdead = 0, cself = 0;
     for (int b = 0; b < 256; ++b) {
-      tg[b] = nid[nxt(r.orig, d.cmap[b])];
-      cdead += tg[b] == 0;
-      cself += tg[b] == self;
-    }
-    r.selfdef = cself > cdead;
-    const uint32_t dflt = r.selfdef ? self : 0u;
-    for (int b = 0; b < 256; ++b)
-      if (tg[b] != dflt) {
+      const uint32_t t = nid[nxt(r.orig, d.cmap[b])];
+      if (t != 0) {
         r.bytes.push_back(static_cast<uint8_t>(b));
-        r.tgt.push_back(tg[b]);
+        r.tgt.push_back(t);
       }
+    }
     n_explicit += r.bytes.size();
   }
 
@@ -224,17 +215,13 @@ re::Status pack_dfa(const re::Dfa& d, PackedDfa* out) {
   p.table.assign(p.n_slots, 0xffffu);
   p.es.assign(p.n_slots, 0);
   p.latch.assign(p.n_slots, kNoPat);
-  auto desc = [&](uint32_t id) -> uint32_t {
-    if (id == 0) return 0;
-    const Row& r = rows[id - 1];
-    return (r.base << 1) | (r.selfdef ? 1u : 0u);
-  };
+  auto base_of = [&](uint32_t id) -> uint32_t { return id == 0 ? 0u : rows[id - 1].base; };
   for (uint32_t i = 0; i < rows.size(); ++i) {
     const Row& r = rows[i];
     const bool multi = i < n_multi;
     for (size_t k = 0; k < r.bytes.size(); ++k) {
       const uint32_t slot = r.base + r.bytes[k];
-      p.table[slot] = r.base | (desc(r.tgt[k]) << 16);
+      p.table[slot] = r.base | (base_of(r.tgt[k]) << 16);
       if (multi && r.tgt[k] > n_multi) {
         // entering the latched region: remember which pattern is still live
         p.latch[slot] = rep[nxt(r.orig, d.cmap[r.bytes[k]])];
@@ -244,7 +231,7 @@ re::Status pack_dfa(const re::Dfa& d, PackedDfa* out) {
   }
   const int s0 = d.start;
   if (cnt[s0] != 0) {
-    p.start_desc = desc(nid[s0]);
+    p.start_base = base_of(nid[s0]);
     if (cnt[s0] == 1) p.start_latch = rep[s0];
   }
   p.region = region;
@@ -256,16 +243,14 @@ re::Status pack_dfa(const re::Dfa& d, PackedDfa* out) {
 }
 
 uint32_t packed_walk(const PackedDfa& p, const uint8_t* s, size_t n) {
-  uint32_t desc = p.start_desc, base = desc >> 1, last = kNoPat;
-  for (size_t i = 0; i < n && desc; ++i) {
+  uint32_t base = p.start_base, last = kNoPat;
+  for (size_t i = 0; i < n && base; ++i) {
     const uint32_t slot = base + s[i];
     const uint32_t e = p.table[slot];
     if (base < p.region) last = slot;
-    if ((e & 0xffffu) == base) desc = e >> 16;
-    else if (!(desc & 1u)) desc = 0;
-    base = desc >> 1;
+    base = (e & 0xffffu) == base ? e >> 16 : 0u;
   }
-  if (!desc) return 0;
+  if (!base) return 0;
   const uint32_t es = p.es[base];
   if (es == kLatchedAccept) return kLatchedAccept | (last == kNoPat ? p.start_latch : p.latch[last]);
   return es;

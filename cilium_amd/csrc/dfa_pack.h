@@ -10,13 +10,11 @@
 // (no byte-class lookup on the critical path):
 //
 //     e = T[base + byte];
-//     if ((e & 0xffff) == base)  desc = e >> 16;        // explicit transition
-//     else if (!(desc & 1))      desc = 0;              // default: dead
-//     /* else default: stay */   base = desc >> 1;
+//     base = (e & 0xffff) == base ? e >> 16 : 0;     // base 0 = dead state
 //
-// desc = (base << 1) | selfdef; base 0 is the dead state.  Each state keeps
-// either "dead" or "self" as its default target; all other transitions are
-// explicit slots (check = owner base).
+// Every non-dead transition is an explicit slot whose check half holds the
+// owner's base; a slot another state owns (or an empty one, check 0xffff)
+// means "dead".  The dead state owns no slot, so it is absorbing.
 //
 // Tail sharing ("latching"): a state from which exactly one pattern can still
 // match is "latched".  Latched states are minimised with binary acceptance,
@@ -33,14 +31,14 @@
 namespace l7m {
 
 constexpr uint32_t kLatchedAccept = 0x80000000u;  // end code: accept the latched pattern
-constexpr uint32_t kMaxDaBase = 32767;            // 15-bit bases (desc is 16 bits)
+constexpr uint32_t kMaxDaBase = 65535 - 256;      // 16-bit bases and slots
 
 struct PackedDfa {
   uint32_t n_slots = 0;          // table length incl. 256 slots of tail padding
-  std::vector<uint32_t> table;   // check | desc << 16; empty slot check = 0xffff
+  std::vector<uint32_t> table;   // check | next_base << 16; empty slot check = 0xffff
   std::vector<uint32_t> es;      // per base: 0 no match, set id (index into sets), or kLatchedAccept
   std::vector<uint32_t> latch;   // per slot: pattern entered by that transition (0xffffffff none)
-  uint32_t start_desc = 0;
+  uint32_t start_base = 0;       // 0 = dead start (nothing can match)
   uint32_t region = 1;           // bases >= region are latched states
   uint32_t start_latch = 0xffffffffu;
   uint32_t nstates = 0;          // packed states incl. dead
@@ -48,7 +46,7 @@ struct PackedDfa {
   std::vector<std::vector<uint32_t>> sets;  // end sets (set id -> sorted pattern ids), set 0 empty
 };
 
-// Returns Ok, or TooBig when a base would exceed kMaxDaBase (caller splits).
+// Returns Ok, or TooBig when a slot would exceed 16 bits (caller splits).
 re::Status pack_dfa(const re::Dfa& d, PackedDfa* out);
 
 // Reference walk of a packed DFA on the host (tests / interpreter parity):

@@ -342,12 +342,34 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   }
 
   // ---- assemble the program -------------------------------------------
-  std::vector<uint32_t> pool;
+  std::vector<uint32_t> pool;  // set pattern lists, remote ids
   auto push_list = [&](const std::vector<uint32_t>& v) -> Span {
     Span s{static_cast<uint32_t>(pool.size()), static_cast<uint32_t>(v.size())};
     pool.insert(pool.end(), v.begin(), v.end());
     return s;
   };
+  // check records (program.h): one per (list, rule)
+  std::vector<uint32_t> cr;
+  auto push_records = [&](const std::vector<uint32_t>& rids) -> Span {
+    Span s{static_cast<uint32_t>(cr.size()), static_cast<uint32_t>(rids.size())};
+    for (uint32_t rid : rids) {
+      cr.push_back(rid);
+      cr.push_back(static_cast<uint32_t>(rule_m[rid].size()) | (remotes[rid].empty() ? 0u : kCrRemote));
+      for (const auto& m : rule_m[rid]) {
+        uint32_t dfa = 0, pat = 0;
+        if (m.fpat != kNone) {
+          auto loc = fp_loc[m.field][m.fpat];
+          dfa = dfa_first[m.field] + loc.first;
+          pat = loc.second;
+        }
+        const uint32_t kind = m.kind == MatchKind::Present ? 1u : 0u;
+        cr.push_back(m.field | (kind << 8) | (dfa << 9));
+        cr.push_back(pat);
+      }
+    }
+    return s;
+  };
+  if (ndfa >= (1u << 23)) return fail(L7M_ETOOBIG, "too many DFA groups");
 
   struct DfaOut {
     const PackedDfa* d;
@@ -361,22 +383,23 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   const uint32_t ndt = static_cast<uint32_t>(all.size());
 
   std::vector<DfaDesc> dd(ndt);
-  std::vector<Span> sets, cands, pcands;
+  std::vector<Span> sets;
+  std::vector<std::vector<Span>> ct(ndt);              // per DFA: [nsets + npats]
+  std::vector<std::vector<uint64_t>> masks(ndt);       // per DFA with npats <= 64
   uint64_t total_states = 0;
   for (uint32_t k = 0; k < ndt; ++k) {
     const PackedDfa& d = *all[k].d;
     std::memset(&dd[k], 0, sizeof(DfaDesc));
-    dd[k].start_desc = d.start_desc;
+    dd[k].start_base = d.start_base;
     dd[k].region = d.region;
     dd[k].start_latch = d.start_latch;
     dd[k].n_slots = d.n_slots;
-    dd[k].set_base = static_cast<uint32_t>(sets.size());
     dd[k].nsets = static_cast<uint32_t>(d.sets.size());
-    dd[k].pcand_base = static_cast<uint32_t>(pcands.size());
     dd[k].npats = all[k].npats;
+    dd[k].set_base = static_cast<uint32_t>(sets.size());
     dd[k].field = all[k].field;
     dd[k].nstates = d.nstates;
-    dd[k].lds_off = kNone;
+    dd[k].lds_table = dd[k].lds_es = dd[k].lds_latch = dd[k].lds_ct = dd[k].lds_mask = kNone;
     total_states += d.nstates;
     for (size_t s = 0; s < d.sets.size(); ++s) {
       sets.push_back(push_list(d.sets[s]));
@@ -388,13 +411,16 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
         }
         std::sort(c.begin(), c.end());
         c.erase(std::unique(c.begin(), c.end()), c.end());
-        cands.push_back(push_list(c));
-      } else {
-        cands.push_back(Span{0, 0});
+        ct[k].push_back(push_records(c));
+      }
+      if (all[k].npats <= 64) {
+        uint64_t m = 0;
+        for (uint32_t p : d.sets[s]) m |= 1ull << p;
+        masks[k].push_back(m);
       }
     }
-    for (uint32_t p = 0; p < all[k].npats; ++p)
-      pcands.push_back(k < ndfa ? push_list(keyed[k][p]) : Span{0, 0});
+    if (k < ndfa)
+      for (uint32_t p = 0; p < all[k].npats; ++p) ct[k].push_back(push_records(keyed[k][p]));
   }
   std::vector<uint32_t> name_field;
   if (has_name) {
@@ -404,29 +430,26 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   for (uint32_t f = 0; f < nf; ++f) {
     fd[f].dfa_first = dfa_first[f];
     fd[f].ndfa = static_cast<uint32_t>(groups[f].size());
-    fd[f].presence = push_list(pres_keyed[f]);
+    fd[f].presence = push_records(pres_keyed[f]);
   }
-  std::vector<Span> rspan(n), rremote(n);
+  std::vector<Span> rremote(n);
   for (size_t i = 0; i < n; ++i) rremote[i] = push_list(remotes[i]);
-  Span zero_span = push_list(zero_list);
-  std::vector<MatcherDesc> md;
-  for (size_t i = 0; i < n; ++i) {
-    rspan[i] = Span{static_cast<uint32_t>(md.size()), static_cast<uint32_t>(rule_m[i].size())};
-    for (const auto& m : rule_m[i]) {
-      MatcherDesc x{m.field, m.kind == MatchKind::Present ? 1u : 0u, kNone, kNone};
-      if (m.fpat != kNone) {
-        auto loc = fp_loc[m.field][m.fpat];
-        x.dfa = dfa_first[m.field] + loc.first;
-        x.pattern = loc.second;
-      }
-      md.push_back(x);
-    }
-  }
+  const Span zero_span = push_records(zero_list);
+  cr.insert(cr.end(), 8, 0u);  // the kernel fetches 8 words per record
 
-  // LDS image: slot tables, hottest first (header names, path, authority,
-  // method, then header values), while they fit the budget.  The rest are
-  // walked from HBM (L2 / MALL resident).
-  const uint64_t lds_budget_words = (opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget) / 4;
+  // ---- LDS image: descriptors always; then, hottest DFA first (header
+  // names, path, authority, method, header values), slot table + u16 end
+  // codes/latches; then candidate tables and set masks, within the budget.
+  const uint64_t budget = (opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget) / 4;
+  uint64_t img = 0;  // image words
+  auto img_take = [&](uint64_t words) {
+    uint64_t o = img;
+    img += (words + 3) & ~uint64_t(3);  // 16-byte granules
+    return static_cast<uint32_t>(o);
+  };
+  const uint32_t lds_dfas = img_take(static_cast<uint64_t>(ndt) * sizeof(DfaDesc) / 4);
+  const uint32_t lds_fields = img_take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
+  const uint32_t lds_name_field = img_take(name_field.size());
   auto hotness = [&](uint32_t k) -> int {
     const uint32_t f = all[k].field;
     if (f == kNone) return 0;
@@ -438,17 +461,23 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   std::vector<uint32_t> order(ndt);
   for (uint32_t k = 0; k < ndt; ++k) order[k] = k;
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hotness(a) < hotness(b); });
-  std::vector<uint32_t> lds_words_of(ndt, kNone);
-  uint64_t lds_words = 0;
   for (uint32_t k : order) {
-    const uint64_t w = (all[k].d->n_slots + 3) & ~uint64_t(3);
-    if (lds_words + w <= lds_budget_words) {
-      lds_words_of[k] = static_cast<uint32_t>(lds_words);
-      lds_words += w;
-    }
+    const PackedDfa& d = *all[k].d;
+    const uint64_t half = (d.n_slots + 1) / 2;
+    const uint64_t need = ((d.n_slots + 3) & ~3ull) + 2 * ((half + 3) & ~3ull);
+    if (img + need > budget || d.sets.size() >= kEs16Latched || all[k].npats >= kEs16Latched) continue;
+    dd[k].lds_table = img_take(d.n_slots);
+    dd[k].lds_es = 2 * img_take(half);
+    dd[k].lds_latch = 2 * img_take(half);
+  }
+  for (uint32_t k : order) {
+    if (k < ndfa && img + ((2 * ct[k].size() + 3) & ~size_t(3)) <= budget)
+      dd[k].lds_ct = img_take(2 * ct[k].size());
+    if (!masks[k].empty() && img + ((2 * masks[k].size() + 3) & ~size_t(3)) <= budget)
+      dd[k].lds_mask = img_take(2 * masks[k].size());
   }
 
-  // layout
+  // ---- program layout ----
   HttpHeader h;
   std::memset(&h, 0, sizeof h);
   uint64_t w = sizeof(HttpHeader) / 4;
@@ -468,52 +497,61 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   h.off_fields = take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
   h.off_name_field = take(name_field.size());
   h.off_sets = take(sets.size() * 2);
-  h.off_cands = take(cands.size() * 2);
-  h.off_pcands = take(pcands.size() * 2);
-  h.off_rules = take(static_cast<uint64_t>(n) * 2);
-  h.off_matchers = take(md.size() * 4);
   h.off_remotes = take(static_cast<uint64_t>(n) * 2);
   h.any_remotes = any_remotes ? 1u : 0u;
   h.zero_list = zero_span;
   h.off_pool = take(pool.size());
-  w = (w + 63) & ~uint64_t(63);  // 256-byte align the table area
-  h.lds_image_off = take(lds_words);
-  h.lds_image_words = static_cast<uint32_t>(lds_words);
+  h.off_cr = take(cr.size());
   for (uint32_t k = 0; k < ndt; ++k) {
-    if (lds_words_of[k] != kNone) {
-      dd[k].lds_off = lds_words_of[k];
-      dd[k].table_off = h.lds_image_off + lds_words_of[k];
-    } else {
-      w = (w + 3) & ~uint64_t(3);
-      dd[k].table_off = take(all[k].d->n_slots);
-    }
-  }
-  for (uint32_t k = 0; k < ndt; ++k) {
+    dd[k].table_off = take(all[k].d->n_slots);
     dd[k].es_off = take(all[k].d->n_slots);
     dd[k].latch_off = take(all[k].d->n_slots);
+    dd[k].ct_off = take(2 * ct[k].size());
   }
+  w = (w + 63) & ~uint64_t(63);  // 256-byte aligned image
+  h.lds_image_off = take(img);
+  h.lds_image_words = static_cast<uint32_t>(img);
+  h.lds_dfas = lds_dfas;
+  h.lds_fields = lds_fields;
+  h.lds_name_field = lds_name_field;
   if (w >= (1ull << 32)) return fail(L7M_ETOOBIG, "program exceeds 16 GiB");
   h.total_words = static_cast<uint32_t>(w);
 
   std::vector<uint32_t> prog(w, 0);
-  std::memcpy(prog.data(), &h, sizeof h);
+  uint32_t* P = prog.data();
+  uint32_t* I = P + h.lds_image_off;
+  uint16_t* I16 = reinterpret_cast<uint16_t*>(I);
+  std::memcpy(P, &h, sizeof h);
   for (uint32_t k = 0; k < ndt; ++k) {
     const PackedDfa& d = *all[k].d;
-    std::memcpy(prog.data() + dd[k].table_off, d.table.data(), d.n_slots * 4ull);
-    std::memcpy(prog.data() + dd[k].es_off, d.es.data(), d.n_slots * 4ull);
-    std::memcpy(prog.data() + dd[k].latch_off, d.latch.data(), d.n_slots * 4ull);
+    std::memcpy(P + dd[k].table_off, d.table.data(), d.n_slots * 4ull);
+    std::memcpy(P + dd[k].es_off, d.es.data(), d.n_slots * 4ull);
+    std::memcpy(P + dd[k].latch_off, d.latch.data(), d.n_slots * 4ull);
+    if (!ct[k].empty()) std::memcpy(P + dd[k].ct_off, ct[k].data(), ct[k].size() * sizeof(Span));
+    if (dd[k].lds_table != kNone) {
+      std::memcpy(I + dd[k].lds_table, d.table.data(), d.n_slots * 4ull);
+      for (uint32_t s = 0; s < d.n_slots; ++s) {
+        I16[dd[k].lds_es + s] = d.es[s] == kLatchedAccept ? static_cast<uint16_t>(kEs16Latched)
+                                                           : static_cast<uint16_t>(d.es[s]);
+        I16[dd[k].lds_latch + s] = d.latch[s] == kNone ? static_cast<uint16_t>(kEs16Latched)
+                                                        : static_cast<uint16_t>(d.latch[s]);
+      }
+    }
+    if (dd[k].lds_ct != kNone) std::memcpy(I + dd[k].lds_ct, ct[k].data(), ct[k].size() * sizeof(Span));
+    if (dd[k].lds_mask != kNone) std::memcpy(I + dd[k].lds_mask, masks[k].data(), masks[k].size() * 8);
   }
-  std::memcpy(prog.data() + h.off_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
-  std::memcpy(prog.data() + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));
-  if (!name_field.empty())
-    std::memcpy(prog.data() + h.off_name_field, name_field.data(), name_field.size() * 4);
-  std::memcpy(prog.data() + h.off_sets, sets.data(), sets.size() * sizeof(Span));
-  std::memcpy(prog.data() + h.off_cands, cands.data(), cands.size() * sizeof(Span));
-  if (!pcands.empty()) std::memcpy(prog.data() + h.off_pcands, pcands.data(), pcands.size() * sizeof(Span));
-  if (n) std::memcpy(prog.data() + h.off_rules, rspan.data(), rspan.size() * sizeof(Span));
-  if (n) std::memcpy(prog.data() + h.off_remotes, rremote.data(), rremote.size() * sizeof(Span));
-  if (!md.empty()) std::memcpy(prog.data() + h.off_matchers, md.data(), md.size() * sizeof(MatcherDesc));
-  if (!pool.empty()) std::memcpy(prog.data() + h.off_pool, pool.data(), pool.size() * 4);
+  std::memcpy(P + h.off_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
+  std::memcpy(I + lds_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
+  std::memcpy(P + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));
+  std::memcpy(I + lds_fields, fd.data(), fd.size() * sizeof(FieldDesc));
+  if (!name_field.empty()) {
+    std::memcpy(P + h.off_name_field, name_field.data(), name_field.size() * 4);
+    std::memcpy(I + lds_name_field, name_field.data(), name_field.size() * 4);
+  }
+  std::memcpy(P + h.off_sets, sets.data(), sets.size() * sizeof(Span));
+  if (n) std::memcpy(P + h.off_remotes, rremote.data(), rremote.size() * sizeof(Span));
+  if (!pool.empty()) std::memcpy(P + h.off_pool, pool.data(), pool.size() * 4);
+  if (!cr.empty()) std::memcpy(P + h.off_cr, cr.data(), cr.size() * 4);
 
   res.program = std::move(prog);
   res.info.proto = L7M_PROTO_HTTP;

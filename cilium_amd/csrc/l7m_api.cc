@@ -87,7 +87,7 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
   if (rs->proto == L7M_PROTO_HTTP) {
     HttpHeader h;
     std::memcpy(&h, rs->program.data(), sizeof h);
-    if (http_lds_bytes(h, 256) > 160 * 1024) return L7M_ETOOBIG;
+    if (http_stage_bytes(h) == 0) return L7M_ETOOBIG;
     e = launch_http(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
                     n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
                     stream, cus);

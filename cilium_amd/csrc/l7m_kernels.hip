@@ -1,17 +1,20 @@
 // l7m_kernels.hip — CDNA4 (gfx950) kernel of the batched HTTP verdict path.
 //
-// One lane per request; a 512-thread workgroup is resident for many tiles of
-// 512 consecutive records (grid-stride).  Per workgroup, once:
-//   * the packed DFA slot tables that fit the LDS budget (the "LDS image",
-//     dfa_pack.h) and the DFA descriptors are copied HBM -> LDS.
-// Per request (lane):
-//   * the record is streamed from HBM with 16-byte non-temporal loads (it is
-//     read exactly once; non-temporal keeps the L2 for the rule tables);
-//   * every referenced field (method / path / authority / header values whose
-//     lower-cased name the header-name DFA recognises) is walked through its
-//     DFA groups: ONE dependent 4-byte LDS read per input byte;
-//   * the end codes select precomputed candidate rule lists; the first rule
-//     (input order) whose remaining matchers hold is the verdict.
+// Persistent layout: one 1024-thread workgroup (16 waves) per CU.  Each wave
+// owns a contiguous range of the batch and consumes it in tiles of up to 64
+// consecutive records (one lane per record):
+//   1. the tile's byte window [off_first, end_last) is copied HBM -> the
+//      wave's LDS stage with coalesced 16-byte non-temporal loads (the arena is
+//      streamed exactly once; the tile is cut short so the window fits);
+//   2. every referenced field (method / path / authority / values of headers
+//      whose lower-cased name the header-name DFA recognises) is walked
+//      through its packed DFA groups (dfa_pack.h): one dependent 4-byte LDS
+//      read per input byte, tables copied to LDS once per workgroup;
+//   3. the end codes select precomputed candidate rule lists (L2-resident);
+//      the first rule (input order) whose other matchers hold is the verdict.
+// A record that is not inside its tile window (non-contiguous offsets, a
+// record larger than the stage, malformed lengths) is evaluated by the same
+// code reading HBM directly.
 // Reference semantics: NetworkPolicyMap::Allowed -> PortNetworkPolicyRule::
 // Matches -> HttpNetworkPolicyRule::Matches -> ConfigUtility::matchHeaders
 // (envoy/cilium_network_policy.h:68-237).
@@ -25,61 +28,77 @@
 namespace l7m {
 namespace {
 
-constexpr uint32_t kBlock = 512;
+constexpr uint32_t kWaves = 16;
+constexpr uint32_t kBlock = 64 * kWaves;
+constexpr uint32_t kMaxStage = 8192;       // bytes of records staged per wave and tile
+constexpr uint32_t kCopyIters = kMaxStage / 1024;
+constexpr uint32_t kLdsBytes = 160 * 1024;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t sel4(const u32x4& v, uint32_t q) {
-  uint32_t r = v.x;
-  r = q == 1u ? v.y : r;
-  r = q == 2u ? v.z : r;
-  r = q == 3u ? v.w : r;
-  return r;
-}
+// Where a record's bytes are read from.
+struct LdsSrc {
+  const uint32_t* w;  // word 0 of the record in the wave's LDS stage
+  __device__ __forceinline__ uint32_t word(uint32_t i) const { return w[i]; }
+  __device__ __forceinline__ uint32_t byte(uint32_t i) const { return reinterpret_cast<const uint8_t*>(w)[i]; }
+};
+struct GlbSrc {
+  const uint32_t* w;  // word 0 of the record in HBM
+  __device__ __forceinline__ uint32_t word(uint32_t i) const { return __builtin_nontemporal_load(w + i); }
+  __device__ __forceinline__ uint32_t byte(uint32_t i) const { return reinterpret_cast<const uint8_t*>(w)[i]; }
+};
 
-// Walk `len` bytes at p through one packed DFA whose slot table is T (LDS or
-// global).  Returns the end code: 0, a set id, or kLatchedBit | pattern.
-template <bool kLds>
-__device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ T, const DfaDesc& dd,
-                                         const uint32_t* __restrict__ prog, const uint8_t* p, uint32_t len) {
-  uint32_t desc = dd.start_desc;
-  uint32_t last = kNone;
-  if (len && desc) {
-    const uint32_t region = dd.region;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const u32x4* cp = reinterpret_cast<const u32x4*>(a & ~uintptr_t(15));
-    uint32_t o = static_cast<uint32_t>(a & 15u);
-    u32x4 ch = __builtin_nontemporal_load(cp);
-    uint32_t w = sel4(ch, o >> 2) >> (8u * (o & 3u));
-    uint32_t base = desc >> 1;
-    for (uint32_t k = 0;;) {
-      const uint32_t slot = base + (w & 0xffu);
-      const uint32_t e = T[slot];
-      if (base < region) last = slot;
-      desc = ((e & 0xffffu) == base) ? (e >> 16) : ((desc & 1u) ? desc : 0u);
-      base = desc >> 1;
-      if (++k == len || desc == 0u) break;
-      ++o;
-      w >>= 8;
-      if ((o & 3u) == 0u) {
-        if (o == 16u) {
-          ++cp;
-          ch = __builtin_nontemporal_load(cp);
-          o = 0;
-        }
-        w = sel4(ch, o >> 2);
-      }
-    }
+// End code of a finished walk (final base, slot of the last transition taken
+// from a multi-pattern state).
+template <bool kLdsTab>
+__device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
+                                             const DfaDesc& dd, uint32_t base, uint32_t last) {
+  if (!base) return 0;
+  if (kLdsTab) {
+    const uint16_t* I16 = reinterpret_cast<const uint16_t*>(img);
+    const uint32_t es = I16[dd.lds_es + base];
+    if (es != kEs16Latched) return es;
+    return kLatchedBit | (last == kNone ? dd.start_latch : I16[dd.lds_latch + last]);
   }
-  if (!desc) return 0;
-  const uint32_t es = prog[dd.es_off + (desc >> 1)];
-  if (es == kLatchedBit) return kLatchedBit | (last == kNone ? dd.start_latch : prog[dd.latch_off + last]);
-  return es;
+  const uint32_t es = prog[dd.es_off + base];
+  if (es != kLatchedBit) return es;
+  return kLatchedBit | (last == kNone ? dd.start_latch : prog[dd.latch_off + last]);
 }
 
-__device__ __forceinline__ uint32_t walk_any(const uint32_t* img, const DfaDesc& dd, const uint32_t* prog,
-                                             const uint8_t* p, uint32_t len) {
-  if (dd.lds_off != kNone) return walk<true>(img + dd.lds_off, dd, prog, p, len);
-  return walk<false>(prog + dd.table_off, dd, prog, p, len);
+// Walk `len` bytes at byte `pos` of the record through one packed DFA
+// (dfa_pack.h): per byte ONE dependent slot-table read,
+//     e = T[base + b];  base = (e & 0xffff) == base ? e >> 16 : 0.
+// The dead state (base 0) is absorbing, so the exit test runs once per 4
+// bytes.  kLdsTab: tables in the LDS image, else in HBM.
+template <bool kLdsTab, class Src>
+__device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
+                                         const DfaDesc& dd, const Src& src, uint32_t pos, uint32_t len) {
+  const uint32_t* __restrict__ T = kLdsTab ? img + dd.lds_table : prog + dd.table_off;
+  const uint32_t region = dd.region;
+  uint32_t base = dd.start_base;
+  uint32_t last = kNone;
+#define L7M_STEP(B)                                        \
+  {                                                        \
+    const uint32_t slot_ = base + (B);                     \
+    const uint32_t e_ = T[slot_];                          \
+    last = base < region ? slot_ : last;                   \
+    base = (e_ & 0xffffu) == base ? (e_ >> 16) : 0u;       \
+  }
+  uint32_t k = 0;
+  if (base) {
+    for (; k + 4 <= len; k += 4) {
+      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
+      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
+      L7M_STEP(b0)
+      L7M_STEP(b1)
+      L7M_STEP(b2)
+      L7M_STEP(b3)
+      if (!base) break;
+    }
+    if (base)
+      for (; k < len; ++k) L7M_STEP(src.byte(pos + k))
+  }
+#undef L7M_STEP
+  return end_code<kLdsTab>(img, prog, dd, base, last);
 }
 
 __device__ __forceinline__ bool set_has(const uint32_t* __restrict__ pool, Span s, uint32_t p) {
@@ -92,6 +111,7 @@ __device__ __forceinline__ bool set_has(const uint32_t* __restrict__ pool, Span 
 }
 
 // Per-wave aggregated counter increment: one atomic per distinct slot.
+// Must be called by every lane of the wave.
 __device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits, uint32_t slot, bool active) {
   uint64_t todo = __ballot(active);
   const uint32_t lane = __lane_id();
@@ -104,212 +124,391 @@ __device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits
   }
 }
 
-template <bool kHits>
+// Per-lane DFA end codes: in registers when the program has few value DFAs
+// (static-index select chains, no scratch), else in an LDS column.
+constexpr uint32_t kRegDfas = 8;
+template <bool kReg>
+struct Codes;
+template <>
+struct Codes<true> {
+  // eight named registers: an array here is turned back into scratch memory
+  uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
+  __device__ __forceinline__ void clear(uint32_t) { r0 = r1 = r2 = r3 = r4 = r5 = r6 = r7 = 0; }
+  __device__ __forceinline__ void set(uint32_t d, uint32_t v) {
+    r0 = d == 0 ? v : r0;
+    r1 = d == 1 ? v : r1;
+    r2 = d == 2 ? v : r2;
+    r3 = d == 3 ? v : r3;
+    r4 = d == 4 ? v : r4;
+    r5 = d == 5 ? v : r5;
+    r6 = d == 6 ? v : r6;
+    r7 = d == 7 ? v : r7;
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t d) const {
+    const uint32_t a = d & 1 ? r1 : r0, b = d & 1 ? r3 : r2, e = d & 1 ? r5 : r4, f = d & 1 ? r7 : r6;
+    const uint32_t lo = d & 2 ? b : a, hi = d & 2 ? f : e;
+    return d & 4 ? hi : lo;
+  }
+};
+template <>
+struct Codes<false> {
+  uint32_t* p;  // LDS, stride kBlock
+  __device__ __forceinline__ void clear(uint32_t n) {
+    for (uint32_t d = 0; d < n; ++d) p[d * kBlock] = 0;
+  }
+  __device__ __forceinline__ void set(uint32_t d, uint32_t v) { p[d * kBlock] = v; }
+  __device__ __forceinline__ uint32_t get(uint32_t d) const { return p[d * kBlock]; }
+};
+
+struct Ctx {
+  const uint32_t* prog;
+  const uint32_t* img;         // LDS image
+  const DfaDesc* dds;          // LDS
+  const FieldDesc* fields;     // LDS
+  const uint32_t* name_field;  // LDS
+  const Span* sets;            // HBM
+  const uint32_t* pool;        // HBM
+  const uint32_t* cr;          // HBM: check records
+  const Span* remotes;         // HBM
+};
+
+template <class Src>
+__device__ __forceinline__ uint32_t walk_dfa(const Ctx& c, uint32_t d, const Src& src, uint32_t pos, uint32_t len) {
+  const DfaDesc& dd = c.dds[d];
+  if (dd.lds_table != kNone) return walk<true>(c.img, c.prog, dd, src, pos, len);
+  return walk<false>(c.img, c.prog, dd, src, pos, len);
+}
+
+// Does end code `code` of DFA d contain pattern p?
+__device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code, uint32_t p) {
+  if (code == 0) return false;
+  if (code & kLatchedBit) return (code & ~kLatchedBit) == p;
+  const DfaDesc& dd = c.dds[d];
+  if (dd.lds_mask != kNone) {
+    const uint32_t* m = c.img + dd.lds_mask + 2u * code;
+    return ((p < 32 ? m[0] >> p : m[1] >> (p - 32)) & 1u) != 0;
+  }
+  return set_has(c.pool, c.sets[dd.set_base + code], p);
+}
+
+// Full evaluation of one record whose first `limit` bytes are readable.
+template <bool kReg, class Src>
+__device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit, uint32_t* col) {
+  Codes<kReg> codes;
+  if constexpr (!kReg) codes.p = col;
+  if (limit < L7M_HTTP_REC_FIXED) return L7M_VERDICT_PARSE_ERROR;
+  const uint32_t w0 = src.word(0), w1 = src.word(1), w2 = src.word(2), w3 = src.word(3), w4 = src.word(4);
+  const uint32_t flags = (w2 >> 16) & 0xffu;
+  const uint32_t nhdr = w2 >> 24;
+  const uint32_t mlen = w3 & 0xffffu, plen = w3 >> 16, alen = w4 & 0xffffu;
+  uint64_t need = L7M_HTTP_REC_FIXED + 4ull * nhdr + mlen + plen + alen;
+  if (need > w0 || ((static_cast<uint64_t>(w0) + 3) & ~3ull) > limit) return L7M_VERDICT_PARSE_ERROR;
+  for (uint32_t j = 0; j < nhdr; ++j) {
+    const uint32_t e = src.word(5 + j);
+    need += (e & 0xffffu) + (e >> 16);
+  }
+  if (need != w0) return L7M_VERDICT_PARSE_ERROR;
+
+  uint64_t present = 0;
+  codes.clear(h.n_dfas);
+  uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
+  auto eval_field = [&](uint32_t f, uint32_t p, uint32_t len) {
+    const FieldDesc& fd = c.fields[f];
+    for (uint32_t k = 0; k < fd.ndfa; ++k) {
+      const uint32_t d = fd.dfa_first + k;
+      codes.set(d, walk_dfa(c, d, src, p, len));
+    }
+  };
+  if (flags & L7M_HTTP_F_METHOD) {
+    present |= 1ull << kFieldMethod;
+    eval_field(kFieldMethod, pos, mlen);
+  }
+  pos += mlen;
+  if (flags & L7M_HTTP_F_PATH) {
+    present |= 1ull << kFieldPath;
+    eval_field(kFieldPath, pos, plen);
+  }
+  pos += plen;
+  if (flags & L7M_HTTP_F_AUTHORITY) {
+    present |= 1ull << kFieldAuthority;
+    eval_field(kFieldAuthority, pos, alen);
+  }
+  pos += alen;
+  if (h.has_name_dfa) {
+    for (uint32_t j = 0; j < nhdr; ++j) {
+      const uint32_t e = src.word(5 + j);
+      const uint32_t nl = e & 0xffffu, vl = e >> 16;
+      const uint32_t code = walk_dfa(c, h.n_dfas, src, pos, nl);
+      uint32_t f = kNone;
+      if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
+      else if (code) f = c.name_field[code];
+      if (f != kNone && !((present >> f) & 1ull)) {  // first occurrence wins
+        present |= 1ull << f;
+        eval_field(f, pos + nl, vl);
+      }
+      pos += nl + vl;
+    }
+  }
+
+  // First matching rule (smallest index) among the keyed candidates: walk
+  // the check-record lists selected by the end codes.
+  uint32_t best = h.always_rule;
+  const uint32_t remote = w1;
+  auto remote_ok = [&](uint32_t rid) -> bool {  // PortNetworkPolicyRule::Matches (h:92-97)
+    const Span rr = c.remotes[rid];
+    uint32_t lo = 0, hi = rr.len;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (c.pool[rr.off + mid] < remote) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo < rr.len && c.pool[rr.off + lo] == remote;
+  };
+  auto scan = [&](Span cl) {
+    uint32_t o = cl.off;
+    for (uint32_t j = 0; j < cl.len; ++j) {
+      // one record: rid, header, up to 3 matchers fetched together
+      uint32_t rw[8];
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) rw[q] = c.cr[o + q];
+      const uint32_t rid = rw[0], nm = rw[1] & 0xffffu;
+      if (rid >= best) break;
+      bool ok = !(rw[1] & kCrRemote) || remote_ok(rid);
+      for (uint32_t q = 0; q < nm && ok; ++q) {
+        const uint32_t a = q < 3 ? (q == 0 ? rw[2] : q == 1 ? rw[4] : rw[6]) : c.cr[o + 2 + 2 * q];
+        const uint32_t pat = q < 3 ? (q == 0 ? rw[3] : q == 1 ? rw[5] : rw[7]) : c.cr[o + 3 + 2 * q];
+        const uint32_t f = a & 0xffu;
+        if (!((present >> f) & 1ull)) ok = false;
+        else if (!((a >> 8) & 1u)) ok = code_has(c, a >> 9, codes.get(a >> 9), pat);
+      }
+      if (ok) {
+        best = rid;
+        break;
+      }
+      o += 2 + 2 * nm;
+    }
+  };
+  auto cand_list = [&](uint32_t d, uint32_t code) -> Span {
+    const DfaDesc& dd = c.dds[d];
+    const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
+    return dd.lds_ct != kNone ? reinterpret_cast<const Span*>(c.img + dd.lds_ct)[idx]
+                              : reinterpret_cast<const Span*>(c.prog + dd.ct_off)[idx];
+  };
+  if constexpr (kReg) {
+    // fetch every candidate-list span first (independent loads in flight together)
+    Span cl[kRegDfas];
+#pragma unroll
+    for (uint32_t d = 0; d < kRegDfas; ++d) {
+      cl[d] = Span{0, 0};
+      const uint32_t code = codes.get(d);
+      if (d < h.n_dfas && code) cl[d] = cand_list(d, code);
+    }
+#pragma unroll
+    for (uint32_t d = 0; d < kRegDfas; ++d)
+      if (cl[d].len) scan(cl[d]);
+  } else {
+    for (uint32_t d = 0; d < h.n_dfas; ++d) {
+      const uint32_t code = codes.get(d);
+      if (!code) continue;
+      const Span cl = cand_list(d, code);
+      if (cl.len) scan(cl);
+    }
+  }
+  for (uint32_t f = 0; f < h.n_fields; ++f)
+    if ((present >> f) & 1ull) {
+      const Span cl = c.fields[f].presence;
+      if (cl.len) scan(cl);
+    }
+  if (h.zero_list.len) scan(h.zero_list);
+
+  if (h.allow_no_l7) return L7M_VERDICT_ALLOW_NO_L7;
+  return best == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(best);
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = __shfl(static_cast<uint32_t>(v), src);
+  const uint32_t hi = __shfl(static_cast<uint32_t>(v >> 32), src);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Per-rule hit counters: none, per-workgroup LDS counters flushed once at the
+// end (small rule sets), or wave-aggregated global atomics.
+enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
+constexpr uint32_t kMaxLdsCounters = 4096;
+
+template <int kHits, bool kReg>
 __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,
                                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                            const uint64_t* __restrict__ offs, uint64_t n,
                                                            int32_t* __restrict__ verdicts,
-                                                           unsigned long long* __restrict__ hits) {
+                                                           unsigned long long* __restrict__ hits, uint32_t stage) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader h = *reinterpret_cast<const HttpHeader*>(prog);
-  const uint32_t ndt = h.n_dfas + h.has_name_dfa;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   uint32_t* img = smem;
-  DfaDesc* dds = reinterpret_cast<DfaDesc*>(smem + h.lds_image_words);
-  uint32_t* sids = smem + h.lds_image_words + 16u * ndt;
-  const uint32_t tid = threadIdx.x;
+  const uint32_t n_ctr = h.n_rules + 2;
+  uint32_t* ctr = smem + h.lds_image_words;  // LDS hit counters (kLdsHits)
+  uint32_t* col = ctr + (kHits == kLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);  // LDS code columns (!kReg)
+  uint8_t* stg = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock)) + wv * (stage + 16u);
   {
     const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
     uint4* l = reinterpret_cast<uint4*>(img);
     for (uint32_t i = tid; i < h.lds_image_words / 4u; i += kBlock) l[i] = g[i];
-    const uint4* gd = reinterpret_cast<const uint4*>(prog + h.off_dfas);
-    uint4* ld = reinterpret_cast<uint4*>(dds);
-    for (uint32_t i = tid; i < 4u * ndt; i += kBlock) ld[i] = gd[i];
+    if (kHits == kLdsHits)
+      for (uint32_t i = tid; i < n_ctr; i += kBlock) ctr[i] = 0;
   }
   __syncthreads();
 
-  const FieldDesc* fields = reinterpret_cast<const FieldDesc*>(prog + h.off_fields);
-  const Span* sets = reinterpret_cast<const Span*>(prog + h.off_sets);
-  const Span* cands = reinterpret_cast<const Span*>(prog + h.off_cands);
-  const Span* pcands = reinterpret_cast<const Span*>(prog + h.off_pcands);
-  const Span* rules = reinterpret_cast<const Span*>(prog + h.off_rules);
-  const MatcherDesc* mds = reinterpret_cast<const MatcherDesc*>(prog + h.off_matchers);
-  const uint32_t* pool = prog + h.off_pool;
-  const uint32_t* name_field = prog + h.off_name_field;
-  const Span* remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
+  Ctx c;
+  c.prog = prog;
+  c.img = img;
+  c.dds = reinterpret_cast<const DfaDesc*>(img + h.lds_dfas);
+  c.fields = reinterpret_cast<const FieldDesc*>(img + h.lds_fields);
+  c.name_field = img + h.lds_name_field;
+  c.sets = reinterpret_cast<const Span*>(prog + h.off_sets);
+  c.pool = prog + h.off_pool;
+  c.cr = prog + h.off_cr;
+  c.remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
+  uint32_t* mycol = col + tid;
 
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
-  for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * kBlock + tid; r < n; r += stride) {
-    const uint64_t off = offs[r];
-    // Malformed record (outside the arena or inconsistent lengths): report
-    // it instead of reading out of bounds.
-    bool bad = (off & 3) || off + L7M_HTTP_REC_FIXED > arena_bytes;
-    const uint8_t* rec = arena + (bad ? 0 : off);
-    const uint32_t* rw = reinterpret_cast<const uint32_t*>(rec);
-    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
-    if (!bad) {
-      w0 = rw[0];
-      w1 = rw[1];
-      w2 = rw[2];
-      w3 = rw[3];
-      w4 = rw[4];
+  // This wave's contiguous share of the batch.
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wv;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  uint64_t cur = n * gw / nw;
+  const uint64_t end = n * (gw + 1) / nw;
+  while (cur < end) {
+    const uint64_t m = end - cur < 64 ? end - cur : 64;
+    uint64_t o = 0, onext = 0;
+    if (lane < m) {
+      o = offs[cur + lane];
+      onext = cur + lane + 1 < n ? offs[cur + lane + 1] : arena_bytes;
     }
-    const uint32_t flags = (w2 >> 16) & 0xffu;
-    const uint32_t nhdr = w2 >> 24;
-    const uint32_t mlen = w3 & 0xffffu, plen = w3 >> 16, alen = w4 & 0xffffu;
-    if (!bad) {
-      uint64_t need = L7M_HTTP_REC_FIXED + 4ull * nhdr + mlen + plen + alen;
-      if (need > w0 || off + ((static_cast<uint64_t>(w0) + 3) & ~3ull) > arena_bytes) {
-        bad = true;
+    const uint64_t o0 = shfl64(o, 0);
+    const uint64_t base = o0 & ~15ull;
+    // Leading run of records that lie, in order, inside a window <= stage.
+    const bool ok = lane < m && (o & 3) == 0 && o >= o0 && onext >= o && onext <= arena_bytes &&
+                    onext - base <= stage;
+    const uint64_t okm = __ballot(ok);
+    const uint32_t k = okm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~okm));
+    const uint32_t bytes = k ? static_cast<uint32_t>(shfl64(onext, k - 1) - base) : 0u;
+    {
+      u32x4 buf[kCopyIters];
+      const u32x4* src = reinterpret_cast<const u32x4*>(arena + base);
+#pragma unroll
+      for (uint32_t it = 0; it < kCopyIters; ++it) {
+        const uint32_t q = it * 64u + lane;
+        if (q * 16u < bytes) buf[it] = __builtin_nontemporal_load(src + q);
+      }
+#pragma unroll
+      for (uint32_t it = 0; it < kCopyIters; ++it) {
+        const uint32_t q = it * 64u + lane;
+        if (q * 16u < bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+      }
+    }
+    wave_sync();
+    const uint32_t take = k ? k : 1u;
+    int32_t v = 0;
+    if (lane < take) {
+      bool done = false;
+      if (lane < k && onext - o >= L7M_HTTP_REC_FIXED) {
+        const LdsSrc s{reinterpret_cast<const uint32_t*>(stg + (o - base))};
+        const uint32_t w0 = s.word(0);
+        if (((static_cast<uint64_t>(w0) + 3) & ~3ull) <= onext - o) {
+          v = eval_record<kReg>(c, h, s, onext - o, mycol);
+          done = true;
+        }
+      }
+      if (!done) {  // outside the staged window: read HBM directly
+        const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
+        const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
+        v = inb ? eval_record<kReg>(c, h, s, arena_bytes - o, mycol) : L7M_VERDICT_PARSE_ERROR;
+      }
+      verdicts[cur + lane] = v;
+    }
+    if (kHits != kNoHits) {
+      uint32_t slot = kNone;
+      if (lane < take && v != L7M_VERDICT_ALLOW_NO_L7)
+        slot = v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u);
+      if (kHits == kLdsHits) {
+        if (slot != kNone) atomicAdd(ctr + slot, 1u);
       } else {
-        for (uint32_t j = 0; j < nhdr; ++j) {
-          const uint32_t e = rw[5 + j];
-          need += (e & 0xffffu) + (e >> 16);
-        }
-        bad = need != w0;
+        count_slot(hits, slot, slot != kNone);
       }
     }
-    if (bad) {
-      verdicts[r] = L7M_VERDICT_PARSE_ERROR;
-      if (kHits) count_slot(hits, 1, true);
-      continue;
-    }
-    uint64_t present = 0;
-    for (uint32_t d = 0; d < h.n_dfas; ++d) sids[d * kBlock + tid] = 0;
-
-    uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
-    auto eval_field = [&](uint32_t f, uint32_t p, uint32_t len) {
-      const FieldDesc fd = fields[f];
-      for (uint32_t k = 0; k < fd.ndfa; ++k) {
-        const uint32_t d = fd.dfa_first + k;
-        sids[d * kBlock + tid] = walk_any(img, dds[d], prog, rec + p, len);
-      }
-    };
-    if (flags & L7M_HTTP_F_METHOD) {
-      present |= 1ull << kFieldMethod;
-      eval_field(kFieldMethod, pos, mlen);
-    }
-    pos += mlen;
-    if (flags & L7M_HTTP_F_PATH) {
-      present |= 1ull << kFieldPath;
-      eval_field(kFieldPath, pos, plen);
-    }
-    pos += plen;
-    if (flags & L7M_HTTP_F_AUTHORITY) {
-      present |= 1ull << kFieldAuthority;
-      eval_field(kFieldAuthority, pos, alen);
-    }
-    pos += alen;
-    if (h.has_name_dfa) {
-      const DfaDesc& nd = dds[h.n_dfas];
-      for (uint32_t j = 0; j < nhdr; ++j) {
-        const uint32_t e = rw[5 + j];
-        const uint32_t nl = e & 0xffffu, vl = e >> 16;
-        const uint32_t code = walk_any(img, nd, prog, rec + pos, nl);
-        uint32_t f = kNone;
-        if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
-        else if (code) f = name_field[code];
-        if (f != kNone && !((present >> f) & 1ull)) {  // first occurrence wins
-          present |= 1ull << f;
-          eval_field(f, pos + nl, vl);
-        }
-        pos += nl + vl;
-      }
-    }
-
-    // First matching rule (smallest index) among the keyed candidates.
-    uint32_t best = h.always_rule;
-    const uint32_t remote = w1;
-    auto verify = [&](uint32_t rid) -> bool {
-      if (!h.any_remotes) {  // PortNetworkPolicyRule::Matches remote check (h:92-97)
-        const Span rr = remotes[rid];
-        if (rr.len) {
-          uint32_t lo = 0, hi = rr.len;
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pool[rr.off + mid] < remote) lo = mid + 1;
-            else hi = mid;
-          }
-          if (lo == rr.len || pool[rr.off + lo] != remote) return false;
-        }
-      }
-      const Span rs = rules[rid];
-      for (uint32_t j = 0; j < rs.len; ++j) {
-        const MatcherDesc m = mds[rs.off + j];
-        if (!((present >> m.field) & 1ull)) return false;
-        if (m.kind == 0) {
-          const uint32_t code = sids[m.dfa * kBlock + tid];
-          if (code == 0) return false;
-          if (code & kLatchedBit) {
-            if ((code & ~kLatchedBit) != m.pattern) return false;
-          } else if (!set_has(pool, sets[dds[m.dfa].set_base + code], m.pattern)) {
-            return false;
-          }
-        }
-      }
-      return true;
-    };
-    auto scan = [&](Span c) {
-      for (uint32_t j = 0; j < c.len; ++j) {
-        const uint32_t rid = pool[c.off + j];
-        if (rid >= best) break;
-        if (verify(rid)) {
-          best = rid;
-          break;
-        }
-      }
-    };
-    for (uint32_t d = 0; d < h.n_dfas; ++d) {
-      const uint32_t code = sids[d * kBlock + tid];
-      if (code & kLatchedBit) scan(pcands[dds[d].pcand_base + (code & ~kLatchedBit)]);
-      else if (code) scan(cands[dds[d].set_base + code]);
-    }
-    for (uint32_t f = 0; f < h.n_fields; ++f)
-      if ((present >> f) & 1ull) scan(fields[f].presence);
-    scan(h.zero_list);
-
-    int32_t v;
-    uint32_t slot;
-    if (h.allow_no_l7) {
-      v = L7M_VERDICT_ALLOW_NO_L7;
-      slot = kNone;
-    } else if (best == kNone) {
-      v = L7M_VERDICT_DENY;
-      slot = 0;
-    } else {
-      v = static_cast<int32_t>(best);
-      slot = best + 2;
-    }
-    verdicts[r] = v;
-    if (kHits) count_slot(hits, slot, slot != kNone);
+    wave_sync();  // the stage is overwritten by the next tile
+    cur += take;
+  }
+  if (kHits == kLdsHits) {
+    __syncthreads();
+    for (uint32_t i = tid; i < n_ctr; i += kBlock)
+      if (ctr[i]) atomicAdd(hits + i, static_cast<unsigned long long>(ctr[i]));
   }
 }
 
 }  // namespace
 
-size_t http_lds_bytes(const HttpHeader& h, uint32_t block) {
-  (void)block;
-  const size_t ndt = h.n_dfas + h.has_name_dfa;
-  return 4u * (static_cast<size_t>(h.lds_image_words) + 16u * ndt + static_cast<size_t>(h.n_dfas) * kBlock);
+size_t http_lds_bytes(const HttpHeader& h, uint32_t stage) {
+  const bool reg = h.n_dfas <= kRegDfas;
+  const size_t ctr = h.n_rules + 2 <= kMaxLdsCounters ? ((h.n_rules + 2 + 3) & ~size_t(3)) : 0;
+  return 4u * (static_cast<size_t>(h.lds_image_words) + ctr + (reg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock)) +
+         static_cast<size_t>(kWaves) * (stage + 16u);
+}
+
+// Bytes of records staged per wave: what is left of the LDS after the tables.
+uint32_t http_stage_bytes(const HttpHeader& h) {
+  const size_t fixed = http_lds_bytes(h, 0) - kWaves * 16u;
+  if (fixed + kWaves * (256u + 16u) > kLdsBytes) return 0;
+  size_t s = (kLdsBytes - fixed) / kWaves - 16u;
+  s &= ~size_t(15);
+  return static_cast<uint32_t>(s > kMaxStage ? kMaxStage : s);
+}
+
+template <int kHits, bool kReg>
+static void launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
+                       uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
+                       unsigned long long* hits, uint32_t stage) {
+  static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((http_eval_kernel<kHits, kReg>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
+                     offs, n, verdicts, hits, stage);
 }
 
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                        const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
                        hipStream_t stream, int num_cus) {
   if (n == 0) return hipSuccess;
-  const size_t lds = http_lds_bytes(h, kBlock);
-  // Workgroups stay resident for many tiles: size the grid to what fits.
-  uint64_t per_cu = lds ? (160u * 1024u) / lds : 4;
-  if (per_cu > 4) per_cu = 4;
-  if (per_cu < 1) per_cu = 1;
-  uint64_t blocks = (n + kBlock - 1) / kBlock;
-  const uint64_t cap = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * per_cu;
-  if (blocks > cap) blocks = cap;
-  if (hits)
-    hipLaunchKernelGGL(http_eval_kernel<true>, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), lds, stream, dprog,
-                       arena, arena_bytes, offs, n, verdicts, hits);
-  else
-    hipLaunchKernelGGL(http_eval_kernel<false>, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), lds, stream, dprog,
-                       arena, arena_bytes, offs, n, verdicts, hits);
+  const uint32_t stage = http_stage_bytes(h);
+  if (stage == 0) return hipErrorInvalidValue;
+  const size_t lds = http_lds_bytes(h, stage);
+  // One resident workgroup per CU; fewer for small batches (>= 8 records per wave).
+  uint64_t blocks = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256);
+  const uint64_t want = (n + 8 * kBlock - 1) / (8 * kBlock);
+  if (want < blocks) blocks = want;
+  const dim3 grid(static_cast<uint32_t>(blocks));
+  const bool reg = h.n_dfas <= kRegDfas;
+  const int mode = !hits ? kNoHits : (h.n_rules + 2 <= kMaxLdsCounters ? kLdsHits : kGlobalHits);
+#define L7M_LAUNCH(M, R) \
+  launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage)
+  if (mode == kNoHits) {
+    if (reg) L7M_LAUNCH(kNoHits, true);
+    else L7M_LAUNCH(kNoHits, false);
+  } else if (mode == kLdsHits) {
+    if (reg) L7M_LAUNCH(kLdsHits, true);
+    else L7M_LAUNCH(kLdsHits, false);
+  } else {
+    if (reg) L7M_LAUNCH(kGlobalHits, true);
+    else L7M_LAUNCH(kGlobalHits, false);
+  }
+#undef L7M_LAUNCH
   return hipGetLastError();
 }
 

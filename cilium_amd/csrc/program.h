@@ -19,7 +19,7 @@
 
 namespace l7m {
 
-constexpr uint32_t kMagicHttp = 0x3248374cu;   // "L7H2" (packed DFA layout)
+constexpr uint32_t kMagicHttp = 0x3348374cu;   // "L7H3" (packed DFA + check records)
 constexpr uint32_t kMagicKafka = 0x504b374cu;  // "L7KP"
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kMaxFields = 64;            // present-mask is one u64 per request
@@ -35,46 +35,52 @@ struct Span {
 };
 
 // One DFA group in packed double-array form (dfa_pack.h).  A walk starts at
-// start_desc and performs, per input byte b,
-//     e = T[base + b];  desc = (e & 0xffff) == base ? e >> 16 : (desc & 1 ? desc : 0)
-// over the u32 slot table T (LDS image when lds_off != kNone, else HBM/L2).
-// The walk's end code is es[base]: 0 (no pattern), a set id (index into this
-// DFA's sets/cands), or kLatchedAccept (0x80000000) meaning "the latched
-// pattern", which is latch[slot of the transition that entered the latched
-// region] (bases >= region), or start_latch.
+// start_base and performs, per input byte b,
+//     e = T[base + b];  base = (e & 0xffff) == base ? e >> 16 : 0   (0 = dead)
+// over the u32 slot table T.  The walk's end code is es[base]: 0 (no
+// pattern), a set id (< nsets), or kLatchedAccept (0x80000000) meaning "the
+// latched pattern" = latch[slot of the transition that entered the latched
+// region (bases >= region)], or start_latch.  Codes are folded into one u32:
+// set id, or kLatchedBit | pattern.
+//
+// Every table has an HBM copy in the program; the hot ones are also part of
+// the LDS image (lds_* != kNone), where es/latch are stored as u16 (0xffff =
+// latched accept / none).
 struct DfaDesc {
-  uint32_t table_off;    // word offset of slot 0 in the program
-  uint32_t lds_off;      // word offset of slot 0 in the LDS image, or kNone
-  uint32_t start_desc;   // (base << 1) | selfdef; 0 = dead (nothing can match)
+  uint32_t table_off;    // program: u32 T[n_slots]
+  uint32_t es_off;       // program: u32 es[n_slots]
+  uint32_t latch_off;    // program: u32 latch[n_slots]
+  uint32_t ct_off;       // program: Span ct[nsets + npats] -> check-record lists
+  uint32_t lds_table;    // LDS image word offset of T, or kNone
+  uint32_t lds_es;       // LDS image u16 index of es16[n_slots], or kNone
+  uint32_t lds_latch;    // LDS image u16 index of latch16[n_slots], or kNone
+  uint32_t lds_ct;       // LDS image word offset of ct, or kNone
+  uint32_t lds_mask;     // LDS image word offset of u64 pattern masks per set (npats <= 64), or kNone
+  uint32_t start_base;   // 0 = dead (nothing can match)
   uint32_t region;       // bases >= region are latched (single-pattern) states
   uint32_t start_latch;  // pattern of a latched start state, else kNone
-  uint32_t es_off;       // u32[n_slots]: end code per base
-  uint32_t latch_off;    // u32[n_slots]: latched pattern per slot
   uint32_t n_slots;
-  uint32_t set_base;     // index of this DFA's set 0 in sets[] / cands[]
   uint32_t nsets;
-  uint32_t pcand_base;   // index of this DFA's pattern 0 in pcands[]
   uint32_t npats;
+  uint32_t set_base;     // index of this DFA's set 0 in sets[] (pattern lists)
   uint32_t field;        // field this DFA evaluates (kNone for the name DFA)
   uint32_t nstates;
-  uint32_t pad[2];
+  uint32_t pad[6];
 };
-static_assert(sizeof(DfaDesc) == 64, "dfa desc is 16 words");
+static_assert(sizeof(DfaDesc) == 96, "dfa desc is 24 words");
 constexpr uint32_t kLatchedBit = 0x80000000u;
+constexpr uint32_t kEs16Latched = 0xffffu;
 
 struct FieldDesc {
   uint32_t dfa_first, ndfa;  // value DFAs of this field (contiguous)
-  Span presence;             // rules keyed on "field present" (sorted)
+  Span presence;             // check-record list keyed on "field present"
 };
 
-// Matcher of a rule: field must be present and, for kind 0, the value DFA
-// `dfa` must have matched local pattern `pattern`.
-struct MatcherDesc {
-  uint32_t field;
-  uint32_t kind;     // 0 = DFA pattern (regex or literal), 1 = presence
-  uint32_t dfa;
-  uint32_t pattern;
-};
+// Check record (u32 words, in the check-record pool; lists are sorted by rid):
+//   [0] rule id   [1] n_matchers | (has_remote_set << 31)
+//   then per matcher: [field | kind << 8 | dfa << 9] [pattern]
+// kind 0 = the DFA's end code must contain `pattern`, 1 = field present.
+constexpr uint32_t kCrRemote = 0x80000000u;
 
 struct HttpHeader {
   uint32_t magic;
@@ -87,18 +93,18 @@ struct HttpHeader {
   uint32_t off_dfas;       // DfaDesc[n_dfas + has_name_dfa]
   uint32_t off_fields;     // FieldDesc[n_fields]
   uint32_t off_name_field; // u32[nsets of name DFA]: set id -> field id (kNone)
-  uint32_t off_sets;       // Span[total sets]: sorted local pattern ids
-  uint32_t off_cands;      // Span[total sets]: sorted rule ids keyed on the set
-  uint32_t off_rules;      // Span[n_rules] into matchers (units of MatcherDesc)
-  uint32_t off_matchers;   // MatcherDesc[]
-  uint32_t off_pool;       // u32 pool
-  uint32_t off_pcands;     // Span[total patterns]: sorted rule ids keyed on the pattern
-  uint32_t lds_image_off;  // program words [off, off + words) are copied to LDS
-  uint32_t lds_image_words;
-  uint32_t total_words;
+  uint32_t off_sets;       // Span[total sets]: sorted local pattern ids (into pool)
+  uint32_t off_cr;         // check-record pool
+  uint32_t off_pool;       // u32 pool (set pattern lists, remote ids)
   uint32_t off_remotes;    // Span[n_rules]: sorted allowed remote ids (len 0 = any)
   uint32_t any_remotes;    // 1 if no rule restricts the remote identity
-  Span zero_list;          // rules without matchers but with a remote set (sorted)
+  Span zero_list;          // check records of rules without matchers but with a remote set
+  uint32_t lds_image_off;  // program words [off, off + words) are copied to LDS
+  uint32_t lds_image_words;
+  uint32_t lds_dfas;       // LDS image word offsets of the DfaDesc / FieldDesc /
+  uint32_t lds_fields;     // name_field copies (always resident)
+  uint32_t lds_name_field;
+  uint32_t total_words;
   uint32_t pad[9];         // header = 32 words
 };
 static_assert(sizeof(HttpHeader) == 128, "header is 32 words");

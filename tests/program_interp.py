@@ -1,10 +1,12 @@
 """Pure-Python interpreter of the compiled HTTP device program (TEST INFRA).
 
 It walks the exact blob libl7match uploads to HBM (cilium_amd/csrc/program.h)
-with the same algorithm as http_eval_kernel, so the rule COMPILER (regex ->
-DFA groups, candidate lists, matcher tables) can be checked against the CPU
-oracle without a GPU.  The kernel itself is checked on the GPU by the -m gpu
-tests.  Small inputs only (pure-Python loops)."""
+with the same algorithm as http_eval_kernel, reading the LDS-image copies of
+the tables where the kernel does (so the u16 end-code / latch images and the
+LDS candidate tables are checked too).  This lets the rule COMPILER (regex ->
+packed DFA groups, check records) be checked against the CPU oracle without a
+GPU; the kernel itself is checked on the GPU by the -m gpu tests.  Small
+inputs only (pure-Python loops)."""
 import struct
 
 import numpy as np
@@ -13,67 +15,80 @@ from cilium_amd import l7match as L
 
 KNONE = 0xFFFFFFFF
 LATCHED = 0x80000000
-HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_dfa off_dfas "
-              "off_fields off_name_field off_sets off_cands off_rules off_matchers off_pool "
-              "off_pcands lds_image_off lds_image_words total_words off_remotes any_remotes "
-              "zero_off zero_len").split()
-DFA_FIELDS = ("table_off lds_off start_desc region start_latch es_off latch_off n_slots set_base nsets "
-              "pcand_base npats field nstates").split()
+ES16_LATCHED = 0xFFFF
+CR_REMOTE = 0x80000000
+HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_dfa off_dfas off_fields "
+              "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
+              "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words").split()
+DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
+              "start_latch n_slots nsets npats set_base field nstates").split()
 
 
 class HttpProgram:
     def __init__(self, prog: np.ndarray):
         self.w = prog.astype(np.uint64).astype(np.int64).tolist()
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
-        assert self.h["magic"] == 0x3248374C
         h = self.h
+        assert h["magic"] == 0x3348374C
+        io = h["lds_image_off"]
+        self.img = self.w[io:io + h["lds_image_words"]]
+        self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
         ndt = h["n_dfas"] + h["has_name_dfa"]
         self.dfas = []
         for k in range(ndt):
-            o = h["off_dfas"] + 16 * k
-            d = dict(zip(DFA_FIELDS, self.w[o:o + len(DFA_FIELDS)]))
-            if d["lds_off"] != KNONE:  # the LDS image is a copy of program words
-                assert d["table_off"] == h["lds_image_off"] + d["lds_off"]
+            o = h["lds_dfas"] + 24 * k  # the kernel reads the LDS copy
+            d = dict(zip(DFA_FIELDS, self.img[o:o + len(DFA_FIELDS)]))
+            g = h["off_dfas"] + 24 * k
+            assert self.w[g:g + 24] == self.img[o:o + 24]
             self.dfas.append(d)
-        self.fields = []
-        for f in range(h["n_fields"]):
-            o = h["off_fields"] + 4 * f
-            self.fields.append(tuple(self.w[o:o + 4]))
-
-    def span(self, off_words, idx):
-        o = off_words + 2 * idx
-        return self.w[o], self.w[o + 1]
-
-    def pool(self, sp):
-        o, n = sp
-        b = self.h["off_pool"] + o
-        return self.w[b:b + n]
+        self.fields = [tuple(self.img[h["lds_fields"] + 4 * f: h["lds_fields"] + 4 * f + 4])
+                       for f in range(h["n_fields"])]
 
     def walk(self, k, data: bytes):
         """Packed double-array walk (cilium_amd/csrc/dfa_pack.h): end code."""
         d = self.dfas[k]
-        T = d["table_off"]
-        desc = d["start_desc"]
-        base = desc >> 1
+        lds = d["lds_table"] != KNONE
+        T, Toff = (self.img, d["lds_table"]) if lds else (self.w, d["table_off"])
+        base = d["start_base"]
         last = KNONE
         for b in data:
-            if not desc:
+            if not base:
                 break
             slot = base + b
-            e = self.w[T + slot]
+            e = T[Toff + slot]
             if base < d["region"]:
                 last = slot
-            if (e & 0xFFFF) == base:
-                desc = e >> 16
-            elif not desc & 1:
-                desc = 0
-            base = desc >> 1
-        if not desc:
+            base = e >> 16 if (e & 0xFFFF) == base else 0
+        if not base:
             return 0
+        if lds:
+            es = self.img16[d["lds_es"] + base]
+            if es != ES16_LATCHED:
+                return es
+            return LATCHED | (d["start_latch"] if last == KNONE else self.img16[d["lds_latch"] + last])
         es = self.w[d["es_off"] + base]
-        if es == LATCHED:
-            return LATCHED | (d["start_latch"] if last == KNONE else self.w[d["latch_off"] + last])
-        return es
+        if es != LATCHED:
+            return es
+        return LATCHED | (d["start_latch"] if last == KNONE else self.w[d["latch_off"] + last])
+
+    def code_has(self, k, code, p):
+        if code == 0:
+            return False
+        if code & LATCHED:
+            return (code & ~LATCHED) == p
+        d = self.dfas[k]
+        if d["lds_mask"] != KNONE:
+            lo, hi = self.img[d["lds_mask"] + 2 * code], self.img[d["lds_mask"] + 2 * code + 1]
+            return bool(((hi << 32 | lo) >> p) & 1)
+        so = self.h["off_sets"] + 2 * (d["set_base"] + code)
+        po, pl = self.w[so], self.w[so + 1]
+        return p in self.w[self.h["off_pool"] + po: self.h["off_pool"] + po + pl]
+
+    def ct(self, k, idx):
+        d = self.dfas[k]
+        if d["lds_ct"] != KNONE:
+            return tuple(self.img[d["lds_ct"] + 2 * idx: d["lds_ct"] + 2 * idx + 2])
+        return tuple(self.w[d["ct_off"] + 2 * idx: d["ct_off"] + 2 * idx + 2])
 
     def eval_record(self, rec: bytes) -> int:
         h = self.h
@@ -84,14 +99,14 @@ class HttpProgram:
         dirs = [struct.unpack_from("<I", rec, 20 + 4 * j)[0] for j in range(nhdr)]
         if 20 + 4 * nhdr + mlen + plen + alen + sum((e & 0xFFFF) + (e >> 16) for e in dirs) != w0:
             return L.VERDICT_PARSE_ERROR
-        sids = [0] * h["n_dfas"]
+        codes = [0] * h["n_dfas"]
         present = 0
         pos = 20 + 4 * nhdr
 
         def eval_field(f, data):
             first, nd, _po, _pl = self.fields[f]
             for k in range(first, first + nd):
-                sids[k] = self.walk(k, data)
+                codes[k] = self.walk(k, data)
 
         for f, flag, ln in ((0, L.F_METHOD, mlen), (1, L.F_PATH, plen), (2, L.F_AUTHORITY, alen)):
             if flags & flag:
@@ -105,48 +120,45 @@ class HttpProgram:
                 if code & LATCHED:
                     f = 3 + (code & ~LATCHED)
                 else:
-                    f = self.w[h["off_name_field"] + code] if code else KNONE
+                    f = self.img[h["lds_name_field"] + code] if code else KNONE
                 if f != KNONE and not (present >> f) & 1:
                     present |= 1 << f
                     eval_field(f, rec[pos + nl:pos + nl + vl])
                 pos += nl + vl
         best = h["always_rule"]
+        cr = h["off_cr"]
 
-        def verify(rid):
-            rr = self.pool(self.span(h["off_remotes"], rid))
-            if rr and remote not in rr:
-                return False
-            mo, mn = self.span(h["off_rules"], rid)
-            for j in range(mn):
-                o = h["off_matchers"] + 4 * (mo + j)
-                fld, kind, dfa, pat = self.w[o:o + 4]
-                if not (present >> fld) & 1:
-                    return False
-                if kind == 0:
-                    code = sids[dfa]
-                    if code == 0:
-                        return False
-                    if code & LATCHED:
-                        if code & ~LATCHED != pat:
-                            return False
-                    elif pat not in self.pool(self.span(h["off_sets"], self.dfas[dfa]["set_base"] + code)):
-                        return False
-            return True
+        def remote_ok(rid):
+            ro, rl = self.w[h["off_remotes"] + 2 * rid: h["off_remotes"] + 2 * rid + 2]
+            return remote in self.w[h["off_pool"] + ro: h["off_pool"] + ro + rl]
 
-        def scan(sp, best):
-            for rid in self.pool(sp):
+        def scan(span, best):
+            o, n = span
+            for _ in range(n):
+                rid, hd = self.w[cr + o], self.w[cr + o + 1]
+                nm = hd & 0xFFFF
                 if rid >= best:
                     break
-                if verify(rid):
+                ok = not (hd & CR_REMOTE) or remote_ok(rid)
+                for q in range(nm):
+                    if not ok:
+                        break
+                    a, pat = self.w[cr + o + 2 + 2 * q], self.w[cr + o + 3 + 2 * q]
+                    if not (present >> (a & 0xFF)) & 1:
+                        ok = False
+                    elif not (a >> 8) & 1:
+                        ok = self.code_has(a >> 9, codes[a >> 9], pat)
+                if ok:
                     return rid
+                o += 2 + 2 * nm
             return best
 
-        for d in range(h["n_dfas"]):
-            code = sids[d]
-            if code & LATCHED:
-                best = scan(self.span(h["off_pcands"], self.dfas[d]["pcand_base"] + (code & ~LATCHED)), best)
-            elif code:
-                best = scan(self.span(h["off_cands"], self.dfas[d]["set_base"] + code), best)
+        for k in range(h["n_dfas"]):
+            code = codes[k]
+            if not code:
+                continue
+            idx = self.dfas[k]["nsets"] + (code & ~LATCHED) if code & LATCHED else code
+            best = scan(self.ct(k, idx), best)
         for f in range(h["n_fields"]):
             if (present >> f) & 1:
                 best = scan((self.fields[f][2], self.fields[f][3]), best)

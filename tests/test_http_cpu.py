@@ -173,6 +173,17 @@ def test_compiler_group_splitting_matches_single_group():
     assert (got == exp).all()
 
 
+@pytest.mark.parametrize("budget", [1, 4096])
+def test_compiler_hbm_resident_tables_match_oracle(budget):
+    """Tables that do not fit the LDS budget are walked from HBM (u32 copies)."""
+    rules = W.rules(2, n_rules=150)
+    arena, offs = W.requests(2, 0, 1500, n_rules=150)
+    rs = L.RuleSet.compile_http(rules, lds_budget_bytes=budget)
+    P = HttpProgram(rs.program())
+    assert any(d["lds_table"] == 0xFFFFFFFF for d in P.dfas)
+    assert (P.eval(arena, offs) == HttpOracle(rules).eval(arena, offs)).all()
+
+
 def test_compiler_edge_cases():
     rules = [
         L.PortRuleHTTP(Headers=["X-Dup"]),                 # presence-only rule

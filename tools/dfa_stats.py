@@ -26,7 +26,7 @@ def main():
         for d in P.dfas:
             name = "names" if d["field"] == KNONE else f"field {d['field']}"
             print(f"   {name:9s} slots {d['n_slots']:6d} states {d['nstates']:6d} region {d['region']:6d} "
-                  f"lds {d['lds_off'] != KNONE}")
+                  f"lds {d['lds_table'] != KNONE} ct_lds {d['lds_ct'] != KNONE}")
 
 
 if __name__ == "__main__":
