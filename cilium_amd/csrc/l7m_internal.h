@@ -10,7 +10,8 @@
 
 namespace l7m {
 
-constexpr uint32_t kDefaultLdsBudget = 64u * 1024u;  // bytes of DFA slot tables in LDS
+constexpr uint32_t kDefaultLdsBudget = 48u * 1024u;  // bytes of DFA tables in the LDS image
+constexpr uint32_t kLdsCtBudget = 24u * 1024u;       // ... including candidate tables
 
 // One getHTTPRule HeaderMatcher (pkg/envoy/server.go:261-320).
 struct HeaderMatcher {
