@@ -23,6 +23,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from cilium_amd import dist as D  # noqa: E402
 from cilium_amd import l7match as L  # noqa: E402
 from cilium_amd import workloads as W  # noqa: E402
 
@@ -114,8 +115,7 @@ def main():
     def step():
         d_hits.zero_()
         rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream)
-        if world > 1:
-            dist.all_reduce(d_hits)
+        D.allreduce_counters(d_hits)  # RCCL (backend "nccl") when world > 1
 
     log(f"rank {rank}: arena {arena_nbytes / 1e9:.2f} GB resident (gen {gen_s:.1f} s, h2d {h2d_s:.2f} s); warmup")
     for _ in range(args.warmup):
@@ -132,8 +132,7 @@ def main():
         ev[i][0].record(stream)
         rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream)
         ev[i][1].record(stream)
-        if world > 1:
-            dist.all_reduce(d_hits)
+        D.allreduce_counters(d_hits)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

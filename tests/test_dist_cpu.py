@@ -1,0 +1,82 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the sharded path: each rank
+evaluates its contiguous shard of the same deterministic workload and the
+per-rule counters are summed with an all-reduce; the result must equal the
+single-process counters.  The verdict computation here is the CPU oracle (the
+checker) because this container has no GPU; the GPU path is the same plumbing
+around l7m_eval_device (bench.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cilium_amd import dist as D
+from cilium_amd import workloads as W
+
+N = 6000
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, cfg, n_rules, out_dir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    from oracle import HttpOracle, KafkaOracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rules = W.rules(cfg, n_rules=n_rules)
+    start, end = D.shard_bounds(N, world, rank)
+    arena, offs = W.requests(cfg, start, end - start, n_rules=n_rules, threads=1)
+    orc = HttpOracle(rules) if cfg != 3 else KafkaOracle(rules)
+    v = orc.eval(arena, offs)
+    ctr = torch.from_numpy(D.counters_from_verdicts(v, len(rules)).view(np.int64).copy())
+    D.allreduce_counters(ctr)
+    np.save(os.path.join(out_dir, f"ctr{rank}.npy"), ctr.numpy())
+    np.save(os.path.join(out_dir, f"v{rank}.npy"), v)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg,n_rules", [(2, 300), (3, 2000)])
+def test_two_rank_sharded_counters_equal_single_process(tmp_path, cfg, n_rules):
+    from oracle import HttpOracle, KafkaOracle
+    mp.start_processes(_worker, args=(2, _free_port(), cfg, n_rules, str(tmp_path)), nprocs=2,
+                       start_method="spawn", join=True)
+    rules = W.rules(cfg, n_rules=n_rules)
+    arena, offs = W.requests(cfg, 0, N, n_rules=n_rules)
+    orc = HttpOracle(rules) if cfg != 3 else KafkaOracle(rules)
+    v = orc.eval(arena, offs)
+    full = D.counters_from_verdicts(v, len(rules)).view(np.int64)
+    for r in range(2):
+        assert (np.load(tmp_path / f"ctr{r}.npy") == full).all()
+    shards = np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(2)])
+    assert (shards == v).all()  # shard invariance of the deterministic workload
+
+
+def test_byte_balanced_bounds_cover_and_balance():
+    arena, offs = W.requests(2, 0, 20000, n_rules=200)
+    nbytes = arena.nbytes - 64
+    for world in (1, 2, 4, 8):
+        b = D.byte_balanced_bounds(offs, nbytes, world)
+        assert b[0][0] == 0 and b[-1][1] == len(offs)
+        assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+        sizes = [(int(offs[e]) if e < len(offs) else nbytes) - int(offs[s]) for s, e in b]
+        assert max(sizes) - min(sizes) <= 2 * 1024
+
+
+def test_counters_from_verdicts_semantics():
+    v = np.array([-1, -2, -3, 0, 2, 2, 0x7FFFFFFF], dtype=np.int32)
+    c = D.counters_from_verdicts(v, 3)
+    assert c.tolist() == [1, 2, 1, 0, 2]
+    assert D.shard_bounds(10, 3, 0) == (0, 3) and D.shard_bounds(10, 3, 2) == (6, 10)
