@@ -68,6 +68,22 @@ def cpu_baseline(cfg, rules, seconds, threads):
                       f"oracle/l7oracle.cc (std::regex_match linear rule scan) on {threads} threads"}
 
 
+def measured_traffic(cfg):
+    """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE
+    passes (tools/traffic.py) of THIS kernel build (matched by .so hash) on
+    the default workload; None when no such measurement exists."""
+    import glob
+    import hashlib
+    with open(L.LIB_PATH, "rb") as f:
+        md5 = hashlib.md5(f.read()).hexdigest()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_cfg{cfg}.json")), reverse=True):
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("so_md5") == md5:
+            return float(t["traffic_bytes"])
+    return None
+
+
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -173,7 +189,8 @@ def main():
                        "parallelism": f"dp{world} (request-sharded, RCCL all-reduce of {rs.n_counters} counters)",
                        "dfa_groups": int(rs.info.n_dfas), "dfa_states": int(rs.info.total_dfa_states)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": measured_traffic(cfg) if not args.requests else None,
                          "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_launch": alg_bytes},
             "counters_ok": hits_total == expect_hits,
             "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
