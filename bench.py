@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--no-hits", action="store_true", help="skip the per-rule counters (diagnostic)")
+    ap.add_argument("--diag", choices=["walk", "copy"], default=None,
+                    help="profiling ablation of the HTTP kernel (verdicts invalid)")
     ap.add_argument("--lds-budget", type=int, default=0, help="bytes of rule tables kept in LDS (0 = default)")
     return ap.parse_args()
 
@@ -126,11 +128,12 @@ def main():
     d_hits = torch.zeros(rs.n_counters, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
 
-    hits_arg = None if args.no_hits else d_hits
+    hits_arg = None if args.no_hits or args.diag else d_hits
+    flags = {None: 0, "walk": L.FLAG_DIAG_WALK_ONLY, "copy": L.FLAG_DIAG_COPY_ONLY}[args.diag]
 
     def step():
         d_hits.zero_()
-        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream)
+        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream, flags)
         D.allreduce_counters(d_hits)  # RCCL (backend "nccl") when world > 1
 
     log(f"rank {rank}: arena {arena_nbytes / 1e9:.2f} GB resident (gen {gen_s:.1f} s, h2d {h2d_s:.2f} s); warmup")
@@ -146,7 +149,7 @@ def main():
     for i in range(args.steps):
         d_hits.zero_()
         ev[i][0].record(stream)
-        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream)
+        rs.eval_device(d_arena, arena_nbytes, d_offs, per_gpu, d_verd, hits_arg, stream.cuda_stream, flags)
         ev[i][1].record(stream)
         D.allreduce_counters(d_hits)
     torch.cuda.synchronize()

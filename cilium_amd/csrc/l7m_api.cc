@@ -77,7 +77,7 @@ int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
 }
 
 int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const void* offs, size_t n, void* verdicts,
-           void* hits, hipStream_t stream) {
+           void* hits, hipStream_t stream, uint32_t flags) {
   auto* rs = const_cast<l7m_ruleset*>(crs);
   const uint32_t* dprog = nullptr;
   int cus = 0;
@@ -90,7 +90,7 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
     if (http_stage_bytes(h) == 0) return L7M_ETOOBIG;
     e = launch_http(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
                     n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
-                    stream, cus);
+                    stream, cus, flags);
   } else if (rs->proto == L7M_PROTO_KAFKA) {
     KafkaHeader h;
     std::memcpy(&h, rs->program.data(), sizeof h);
@@ -259,16 +259,15 @@ size_t l7m_pack_http(const l7m_http_request* reqs, size_t n, uint8_t* arena, siz
 int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes,
                     const void* d_offsets, size_t n, void* d_verdicts, void* d_hits,
                     void* hip_stream, uint32_t flags) {
-  (void)flags;
   if (!rs || (n && (!d_arena || !d_offsets || !d_verdicts))) return L7M_EINVAL;
   // The kernels stream records with aligned 16-byte loads.
   if (reinterpret_cast<uintptr_t>(d_arena) & 15) return L7M_EINVAL;
-  return launch(rs, d_arena, arena_bytes, d_offsets, n, d_verdicts, d_hits, static_cast<hipStream_t>(hip_stream));
+  return launch(rs, d_arena, arena_bytes, d_offsets, n, d_verdicts, d_hits, static_cast<hipStream_t>(hip_stream),
+                flags);
 }
 
 int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
              const uint64_t* offsets, size_t n, int32_t* verdicts, uint64_t* hits, uint32_t flags) {
-  (void)flags;
   if (!rs || (n && (!arena || !offsets || !verdicts))) return L7M_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return L7M_EDEVICE;
@@ -297,7 +296,7 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
             hipMemcpyAsync(doff, offsets, n * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
             (!hits || hipMemsetAsync(dh, 0, nctr * 8, st) == hipSuccess);
   if (!ok) rc = L7M_EDEVICE;
-  if (rc == L7M_OK) rc = launch(rs, da, arena_bytes, doff, n, dv, dh, st);
+  if (rc == L7M_OK) rc = launch(rs, da, arena_bytes, doff, n, dv, dh, st, flags);
   if (rc == L7M_OK &&
       hipMemcpyAsync(verdicts, dv, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
     rc = L7M_EDEVICE;

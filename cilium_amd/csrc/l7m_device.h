@@ -15,7 +15,7 @@ size_t http_lds_bytes(const HttpHeader& h, uint32_t stage);
 uint32_t http_stage_bytes(const HttpHeader& h);
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                       unsigned long long* hits, hipStream_t stream, int num_cus);
+                       unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags);
 
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena,
                         uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,

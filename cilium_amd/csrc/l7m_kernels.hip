@@ -192,7 +192,9 @@ __device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code
 }
 
 // Full evaluation of one record whose first `limit` bytes are readable.
-template <bool kReg, class Src>
+// kAblate (diagnostic builds selected by L7M_FLAG_DIAG_*; verdicts invalid):
+// 1 = stop after the DFA walks, 2 = stop after record validation.
+template <bool kReg, int kAblate, class Src>
 __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit, uint32_t* col) {
   Codes<kReg> codes;
   if constexpr (!kReg) codes.p = col;
@@ -209,6 +211,7 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   }
   if (need != w0) return L7M_VERDICT_PARSE_ERROR;
 
+  if constexpr (kAblate == 2) return static_cast<int32_t>(w0 & 7u);
   uint64_t present = 0;
   codes.clear(h.n_dfas);
   uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
@@ -250,6 +253,11 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     }
   }
 
+  if constexpr (kAblate == 1) {
+    uint32_t acc = static_cast<uint32_t>(present);
+    for (uint32_t d = 0; d < h.n_dfas; ++d) acc += codes.get(d);
+    return static_cast<int32_t>(acc & 7u);
+  }
   // First matching rule (smallest index) among the keyed candidates: walk
   // the check-record lists selected by the end codes.
   uint32_t best = h.always_rule;
@@ -341,7 +349,7 @@ __device__ __forceinline__ void wave_sync() {
 enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
 constexpr uint32_t kMaxLdsCounters = 4096;
 
-template <int kHits, bool kReg>
+template <int kHits, bool kReg, int kAblate>
 __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,
                                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                            const uint64_t* __restrict__ offs, uint64_t n,
@@ -419,14 +427,14 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
         const LdsSrc s{reinterpret_cast<const uint32_t*>(stg + (o - base))};
         const uint32_t w0 = s.word(0);
         if (((static_cast<uint64_t>(w0) + 3) & ~3ull) <= onext - o) {
-          v = eval_record<kReg>(c, h, s, onext - o, mycol);
+          v = eval_record<kReg, kAblate>(c, h, s, onext - o, mycol);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: read HBM directly
         const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
         const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-        v = inb ? eval_record<kReg>(c, h, s, arena_bytes - o, mycol) : L7M_VERDICT_PARSE_ERROR;
+        v = inb ? eval_record<kReg, kAblate>(c, h, s, arena_bytes - o, mycol) : L7M_VERDICT_PARSE_ERROR;
       }
       verdicts[cur + lane] = v;
     }
@@ -468,23 +476,23 @@ uint32_t http_stage_bytes(const HttpHeader& h) {
   return static_cast<uint32_t>(s > kMaxStage ? kMaxStage : s);
 }
 
-template <int kHits, bool kReg>
+template <int kHits, bool kReg, int kAblate = 0>
 static void launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, uint32_t stage) {
   static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     attr_set = true;
   }
-  hipLaunchKernelGGL((http_eval_kernel<kHits, kReg>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
+  hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
                      offs, n, verdicts, hits, stage);
 }
 
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                        const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
-                       hipStream_t stream, int num_cus) {
+                       hipStream_t stream, int num_cus, uint32_t flags) {
   if (n == 0) return hipSuccess;
   const uint32_t stage = http_stage_bytes(h);
   if (stage == 0) return hipErrorInvalidValue;
@@ -495,6 +503,14 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   if (want < blocks) blocks = want;
   const dim3 grid(static_cast<uint32_t>(blocks));
   const bool reg = h.n_dfas <= kRegDfas;
+  if (flags & (L7M_FLAG_DIAG_WALK_ONLY | L7M_FLAG_DIAG_COPY_ONLY)) {  // diagnostic ablations
+    if (!reg) return hipErrorInvalidValue;
+    if (flags & L7M_FLAG_DIAG_COPY_ONLY)
+      launch_one<kNoHits, true, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
+    else
+      launch_one<kNoHits, true, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
+    return hipGetLastError();
+  }
   const int mode = !hits ? kNoHits : (h.n_rules + 2 <= kMaxLdsCounters ? kLdsHits : kGlobalHits);
 #define L7M_LAUNCH(M, R) \
   launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage)

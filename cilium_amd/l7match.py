@@ -40,6 +40,9 @@ VERDICT_ALLOW_NO_L7 = 0x7FFFFFFF
 DIALECT_ENVOY_ECMA_FULL = 0
 DIALECT_RE2_SEARCH = 1
 
+FLAG_DIAG_WALK_ONLY = 0x40000000  # profiling ablations: verdicts NOT valid
+FLAG_DIAG_COPY_ONLY = 0x80000000
+
 PROTO_HTTP = 1
 PROTO_KAFKA = 2
 
@@ -375,14 +378,14 @@ class RuleSet:
         return verdicts
 
     def eval_device(self, d_arena, arena_bytes: int, d_offsets, n: int, d_verdicts,
-                    d_hits=None, stream=None) -> None:
+                    d_hits=None, stream=None, flags: int = 0) -> None:
         """Device pointers (ints or torch tensors) -> enqueue on `stream` (int handle)."""
         def ptr(x):
             if x is None:
                 return None
             return x.data_ptr() if hasattr(x, "data_ptr") else int(x)
         rc = _lib.l7m_eval_device(self._h, ptr(d_arena), arena_bytes, ptr(d_offsets), n,
-                                  ptr(d_verdicts), ptr(d_hits), stream, 0)
+                                  ptr(d_verdicts), ptr(d_hits), stream, flags)
         if rc != L7M_OK:
             raise L7Error(rc, "l7m_eval_device failed")
 

@@ -192,10 +192,16 @@ size_t l7m_http_record_size(const l7m_http_request* req);
 size_t l7m_pack_http(const l7m_http_request* reqs, size_t n, uint8_t* arena, size_t cap,
                      uint64_t* offsets);
 
+/* ---- evaluation flags ------------------------------------------------------
+ * 0 for normal use.  The DIAG flags select profiling ablations of the HTTP
+ * kernel whose verdicts are NOT valid (used by bench.py --diag). */
+#define L7M_FLAG_DIAG_WALK_ONLY 0x40000000u  /* stop after the DFA walks       */
+#define L7M_FLAG_DIAG_COPY_ONLY 0x80000000u  /* stop after staging/validation  */
+
 /* ---- evaluation (hot path) ----------------------------------------------
  * verdicts: int32[n].  rule_hits: NULL or uint64[n_rules + 2], ACCUMULATED
  * (not cleared): [0] denies, [1] parse errors + unsupported, [2 + i] requests
- * allowed by rule i.  flags: reserved, 0.
+ * allowed by rule i.  flags: 0 (or L7M_FLAG_DIAG_* for profiling).
  */
 int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
              const uint64_t* rec_offsets, size_t n, int32_t* verdicts, uint64_t* rule_hits,
