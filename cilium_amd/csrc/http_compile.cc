@@ -400,6 +400,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     dd[k].field = all[k].field;
     dd[k].nstates = d.nstates;
     dd[k].lds_table = dd[k].lds_es = dd[k].lds_latch = dd[k].lds_ct = dd[k].lds_mask = kNone;
+    dd[k].lds_ctmask = kNone;
     total_states += d.nstates;
     for (size_t s = 0; s < d.sets.size(); ++s) {
       sets.push_back(push_list(d.sets[s]));
@@ -450,6 +451,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   const uint32_t lds_dfas = img_take(static_cast<uint64_t>(ndt) * sizeof(DfaDesc) / 4);
   const uint32_t lds_fields = img_take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
   const uint32_t lds_name_field = img_take(name_field.size());
+  for (uint32_t k = 0; k < ndfa; ++k) dd[k].lds_ctmask = img_take((ct[k].size() + 31) / 32);
   auto hotness = [&](uint32_t k) -> int {
     const uint32_t f = all[k].field;
     if (f == kNone) return 0;
@@ -479,8 +481,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
       dd[k].lds_mask = img_take(2 * masks[k].size());
   }
   for (uint32_t k : order) {
-    if (k < ndfa && img + ((2 * ct[k].size() + 3) & ~size_t(3)) <= ct_budget)
-      dd[k].lds_ct = img_take(2 * ct[k].size());
+    if (k < ndfa && img + ((16 * ct[k].size() + 3) & ~size_t(3)) <= ct_budget)
+      dd[k].lds_ct = img_take(16 * ct[k].size());
   }
 
   // ---- program layout ----
@@ -512,7 +514,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     dd[k].table_off = take(all[k].d->n_slots);
     dd[k].es_off = take(all[k].d->n_slots);
     dd[k].latch_off = take(all[k].d->n_slots);
-    dd[k].ct_off = take(2 * ct[k].size());
+    dd[k].ct_off = take(16 * ct[k].size());
   }
   w = (w + 63) & ~uint64_t(63);  // 256-byte aligned image
   h.lds_image_off = take(img);
@@ -533,7 +535,20 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     std::memcpy(P + dd[k].table_off, d.table.data(), d.n_slots * 4ull);
     std::memcpy(P + dd[k].es_off, d.es.data(), d.n_slots * 4ull);
     std::memcpy(P + dd[k].latch_off, d.latch.data(), d.n_slots * 4ull);
-    if (!ct[k].empty()) std::memcpy(P + dd[k].ct_off, ct[k].data(), ct[k].size() * sizeof(Span));
+    std::vector<CandEntry> ce(ct[k].size());
+    std::memset(ce.data(), 0, ce.size() * sizeof(CandEntry));
+    for (size_t i = 0; i < ct[k].size(); ++i) {
+      const Span sp = ct[k][i];
+      ce[i].len = sp.len;
+      ce[i].off = sp.off;
+      if (sp.len) {
+        const uint32_t nm = cr[sp.off + 1] & 0xffffu;
+        const uint32_t words = 2 + 2 * std::min(nm, kCandInlineMatchers);
+        std::memcpy(ce[i].rec, cr.data() + sp.off, words * 4);
+        I[dd[k].lds_ctmask + i / 32] |= 1u << (i % 32);
+      }
+    }
+    if (!ce.empty()) std::memcpy(P + dd[k].ct_off, ce.data(), ce.size() * sizeof(CandEntry));
     if (dd[k].lds_table != kNone) {
       std::memcpy(I + dd[k].lds_table, d.table.data(), d.n_slots * 4ull);
       for (uint32_t s = 0; s < d.n_slots; ++s) {
@@ -543,7 +558,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
                                                         : static_cast<uint16_t>(d.latch[s]);
       }
     }
-    if (dd[k].lds_ct != kNone) std::memcpy(I + dd[k].lds_ct, ct[k].data(), ct[k].size() * sizeof(Span));
+    if (dd[k].lds_ct != kNone) std::memcpy(I + dd[k].lds_ct, ce.data(), ce.size() * sizeof(CandEntry));
     if (dd[k].lds_mask != kNone) std::memcpy(I + dd[k].lds_mask, masks[k].data(), masks[k].size() * 8);
   }
   std::memcpy(P + h.off_dfas, dd.data(), dd.size() * sizeof(DfaDesc));

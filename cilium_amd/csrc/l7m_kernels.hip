@@ -296,31 +296,38 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
       o += 2 + 2 * nm;
     }
   };
-  auto cand_list = [&](uint32_t d, uint32_t code) -> Span {
+  // Candidates of each DFA end code: one 64-byte CandEntry whose first check
+  // record is inline; longer lists fall back to the pool scan.
+  auto check_inline = [&](const uint32_t* e) {  // e -> CandEntry (LDS or HBM)
+    const u32x4 q0 = reinterpret_cast<const u32x4*>(e)[0];  // len, off, rid, hdr
+    const uint32_t len = q0.x, rid = q0.z, hd = q0.w, nm = hd & 0xffffu;
+    if (len == 1 && nm <= kCandInlineMatchers) {
+      if (rid >= best) return;
+      const u32x4 q1 = reinterpret_cast<const u32x4*>(e)[1];
+      const u32x4 q2 = reinterpret_cast<const u32x4*>(e)[2];
+      const uint32_t ma[4] = {q1.x, q1.z, q2.x, q2.z}, mp[4] = {q1.y, q1.w, q2.y, q2.w};
+      bool ok = !(hd & kCrRemote) || remote_ok(rid);
+#pragma unroll
+      for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {
+        if (q < nm && ok) {
+          const uint32_t a = ma[q];
+          if (!((present >> (a & 0xffu)) & 1ull)) ok = false;
+          else if (!((a >> 8) & 1u)) ok = code_has(c, a >> 9, codes.get(a >> 9), mp[q]);
+        }
+      }
+      if (ok) best = rid;
+    } else {
+      scan(Span{q0.y, len});
+    }
+  };
+  for (uint32_t d = 0; d < h.n_dfas; ++d) {
+    const uint32_t code = codes.get(d);
+    if (!code) continue;
     const DfaDesc& dd = c.dds[d];
     const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
-    return dd.lds_ct != kNone ? reinterpret_cast<const Span*>(c.img + dd.lds_ct)[idx]
-                              : reinterpret_cast<const Span*>(c.prog + dd.ct_off)[idx];
-  };
-  if constexpr (kReg) {
-    // fetch every candidate-list span first (independent loads in flight together)
-    Span cl[kRegDfas];
-#pragma unroll
-    for (uint32_t d = 0; d < kRegDfas; ++d) {
-      cl[d] = Span{0, 0};
-      const uint32_t code = codes.get(d);
-      if (d < h.n_dfas && code) cl[d] = cand_list(d, code);
-    }
-#pragma unroll
-    for (uint32_t d = 0; d < kRegDfas; ++d)
-      if (cl[d].len) scan(cl[d]);
-  } else {
-    for (uint32_t d = 0; d < h.n_dfas; ++d) {
-      const uint32_t code = codes.get(d);
-      if (!code) continue;
-      const Span cl = cand_list(d, code);
-      if (cl.len) scan(cl);
-    }
+    if (!((c.img[dd.lds_ctmask + (idx >> 5)] >> (idx & 31u)) & 1u)) continue;  // no candidates
+    if (dd.lds_ct != kNone) check_inline(c.img + dd.lds_ct + 16u * idx);
+    else check_inline(c.prog + dd.ct_off + 16u * idx);
   }
   for (uint32_t f = 0; f < h.n_fields; ++f)
     if ((present >> f) & 1ull) {

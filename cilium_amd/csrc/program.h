@@ -50,11 +50,11 @@ struct DfaDesc {
   uint32_t table_off;    // program: u32 T[n_slots]
   uint32_t es_off;       // program: u32 es[n_slots]
   uint32_t latch_off;    // program: u32 latch[n_slots]
-  uint32_t ct_off;       // program: Span ct[nsets + npats] -> check-record lists
+  uint32_t ct_off;       // program: CandEntry ct[nsets + npats] (16 words each)
   uint32_t lds_table;    // LDS image word offset of T, or kNone
   uint32_t lds_es;       // LDS image u16 index of es16[n_slots], or kNone
   uint32_t lds_latch;    // LDS image u16 index of latch16[n_slots], or kNone
-  uint32_t lds_ct;       // LDS image word offset of ct, or kNone
+  uint32_t lds_ct;       // LDS image word offset of ct (CandEntry[]), or kNone
   uint32_t lds_mask;     // LDS image word offset of u64 pattern masks per set (npats <= 64), or kNone
   uint32_t start_base;   // 0 = dead (nothing can match)
   uint32_t region;       // bases >= region are latched (single-pattern) states
@@ -65,9 +65,23 @@ struct DfaDesc {
   uint32_t set_base;     // index of this DFA's set 0 in sets[] (pattern lists)
   uint32_t field;        // field this DFA evaluates (kNone for the name DFA)
   uint32_t nstates;
-  uint32_t pad[6];
+  uint32_t lds_ctmask;   // LDS image word offset of a bitmask: ct entry i has candidates
+  uint32_t pad[5];
 };
 static_assert(sizeof(DfaDesc) == 96, "dfa desc is 24 words");
+
+// Candidate entry of one end code (16 words): the keyed rules' check records
+// (sorted by rule id) live in the check-record pool at [off, len records);
+// the first record is also inlined when it has <= kCandInlineMatchers
+// matchers, so the common single-candidate case costs one 64-byte read.
+constexpr uint32_t kCandInlineMatchers = 4;
+struct CandEntry {
+  uint32_t len;       // number of check records (0 = no candidate)
+  uint32_t off;       // word offset of the first record in the pool
+  uint32_t rec[10];   // first record: rid, header, up to 4 x (matcher, pattern)
+  uint32_t pad[4];
+};
+static_assert(sizeof(CandEntry) == 64, "cand entry is 16 words");
 constexpr uint32_t kLatchedBit = 0x80000000u;
 constexpr uint32_t kEs16Latched = 0xffffu;
 

@@ -21,7 +21,7 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
-              "start_latch n_slots nsets npats set_base field nstates").split()
+              "start_latch n_slots nsets npats set_base field nstates lds_ctmask").split()
 
 
 class HttpProgram:
@@ -85,10 +85,22 @@ class HttpProgram:
         return p in self.w[self.h["off_pool"] + po: self.h["off_pool"] + po + pl]
 
     def ct(self, k, idx):
+        """Candidate list (pool offset, record count) of end-code index idx;
+        checks the LDS presence bit and the inlined first record."""
         d = self.dfas[k]
+        bit = (self.img[d["lds_ctmask"] + (idx >> 5)] >> (idx & 31)) & 1
         if d["lds_ct"] != KNONE:
-            return tuple(self.img[d["lds_ct"] + 2 * idx: d["lds_ct"] + 2 * idx + 2])
-        return tuple(self.w[d["ct_off"] + 2 * idx: d["ct_off"] + 2 * idx + 2])
+            e = self.img[d["lds_ct"] + 16 * idx: d["lds_ct"] + 16 * idx + 16]
+        else:
+            e = self.w[d["ct_off"] + 16 * idx: d["ct_off"] + 16 * idx + 16]
+        n, off = e[0], e[1]
+        assert bit == (1 if n else 0)
+        if n:
+            cr = self.h["off_cr"] + off
+            nm = self.w[cr + 1] & 0xFFFF
+            k_in = 2 + 2 * min(nm, 4)
+            assert e[2:2 + k_in] == self.w[cr:cr + k_in]
+        return off, n
 
     def eval_record(self, rec: bytes) -> int:
         h = self.h
