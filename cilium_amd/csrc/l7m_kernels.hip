@@ -391,42 +391,73 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
   c.remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
   uint32_t* mycol = col + tid;
 
-  // This wave's contiguous share of the batch.
+  // This wave's contiguous share of the batch, consumed in tiles of <= 64
+  // records.  Software pipeline per wave: while tile t is evaluated from the
+  // LDS stage, tile t+1's bytes and tile t+2's offsets are already in flight.
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wv;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  uint64_t cur = n * gw / nw;
   const uint64_t end = n * (gw + 1) / nw;
-  while (cur < end) {
-    const uint64_t m = end - cur < 64 ? end - cur : 64;
-    uint64_t o = 0, onext = 0;
-    if (lane < m) {
-      o = offs[cur + lane];
-      onext = cur + lane + 1 < n ? offs[cur + lane + 1] : arena_bytes;
+  struct Tile {
+    uint64_t cur, o, onext, base;
+    uint32_t k, bytes, take;
+  };
+  auto load_offs = [&](uint64_t cur, uint64_t* o, uint64_t* onext) {
+    *o = 0;
+    *onext = 0;
+    if (cur < end && lane < end - cur) {
+      *o = offs[cur + lane];
+      *onext = cur + lane + 1 < n ? offs[cur + lane + 1] : arena_bytes;
     }
+  };
+  auto plan = [&](uint64_t cur, uint64_t o, uint64_t onext) -> Tile {
+    Tile t;
+    t.cur = cur;
+    t.o = o;
+    t.onext = onext;
+    if (cur >= end) {
+      t.base = 0;
+      t.k = t.bytes = t.take = 0;
+      return t;
+    }
+    const uint64_t m = end - cur < 64 ? end - cur : 64;
     const uint64_t o0 = shfl64(o, 0);
-    const uint64_t base = o0 & ~15ull;
+    t.base = o0 & ~15ull;
     // Leading run of records that lie, in order, inside a window <= stage.
     const bool ok = lane < m && (o & 3) == 0 && o >= o0 && onext >= o && onext <= arena_bytes &&
-                    onext - base <= stage;
+                    onext - t.base <= stage;
     const uint64_t okm = __ballot(ok);
-    const uint32_t k = okm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~okm));
-    const uint32_t bytes = k ? static_cast<uint32_t>(shfl64(onext, k - 1) - base) : 0u;
-    {
-      u32x4 buf[kCopyIters];
-      const u32x4* src = reinterpret_cast<const u32x4*>(arena + base);
+    t.k = okm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~okm));
+    t.bytes = t.k ? static_cast<uint32_t>(shfl64(onext, t.k - 1) - t.base) : 0u;
+    t.take = t.k ? t.k : 1u;
+    return t;
+  };
+  u32x4 buf[kCopyIters];
+  auto issue_bytes = [&](const Tile& t) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
 #pragma unroll
-      for (uint32_t it = 0; it < kCopyIters; ++it) {
-        const uint32_t q = it * 64u + lane;
-        if (q * 16u < bytes) buf[it] = __builtin_nontemporal_load(src + q);
-      }
+    for (uint32_t it = 0; it < kCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
+    }
+  };
+  uint64_t o1, n1, o2, n2;
+  load_offs(n * gw / nw, &o1, &n1);
+  Tile t = plan(n * gw / nw, o1, n1);
+  issue_bytes(t);
+  load_offs(t.cur + t.take, &o2, &n2);
+  while (t.cur < end) {
 #pragma unroll
-      for (uint32_t it = 0; it < kCopyIters; ++it) {
-        const uint32_t q = it * 64u + lane;
-        if (q * 16u < bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
-      }
+    for (uint32_t it = 0; it < kCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
     }
     wave_sync();
-    const uint32_t take = k ? k : 1u;
+    const Tile t2 = plan(t.cur + t.take, o2, n2);
+    issue_bytes(t2);
+    load_offs(t2.cur + t2.take, &o2, &n2);
+
+    const uint64_t o = t.o, onext = t.onext, base = t.base;
+    const uint32_t k = t.k, take = t.take;
     int32_t v = 0;
     if (lane < take) {
       bool done = false;
@@ -443,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
         const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
         v = inb ? eval_record<kReg, kAblate>(c, h, s, arena_bytes - o, mycol) : L7M_VERDICT_PARSE_ERROR;
       }
-      verdicts[cur + lane] = v;
+      verdicts[t.cur + lane] = v;
     }
     if (kHits != kNoHits) {
       uint32_t slot = kNone;
@@ -456,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
       }
     }
     wave_sync();  // the stage is overwritten by the next tile
-    cur += take;
+    t = t2;
   }
   if (kHits == kLdsHits) {
     __syncthreads();
