@@ -25,10 +25,14 @@
 #include "l7m_device.h"
 #include "program.h"
 
+#ifndef L7M_HTTP_WAVES
+#define L7M_HTTP_WAVES 16  // waves per workgroup (one workgroup per CU)
+#endif
+
 namespace l7m {
 namespace {
 
-constexpr uint32_t kWaves = 16;
+constexpr uint32_t kWaves = L7M_HTTP_WAVES;
 constexpr uint32_t kBlock = 64 * kWaves;
 constexpr uint32_t kMaxStage = 8192;       // bytes of records staged per wave and tile
 constexpr uint32_t kCopyIters = kMaxStage / 1024;

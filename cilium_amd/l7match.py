@@ -21,7 +21,8 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libl7match.so")
+# L7M_LIB: alternative in-tree build of the same ABI (kernel experiments).
+LIB_PATH = os.environ.get("L7M_LIB") or os.path.join(_HERE, "libl7match.so")
 
 L7M_OK = 0
 L7M_EINVAL = -1
