@@ -18,6 +18,8 @@
 //      (the max term is the rule that removes the last uncovered topic).
 // Verdicts: -1 deny, -2 ReadRequest error, -3 compressed message set, i >= 0
 // allowed by rule i.
+// Records are staged through LDS per wave tile exactly like the HTTP kernel
+// (l7m_kernels.hip); the decoder then reads LDS.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -228,16 +230,16 @@ __device__ void cover_topic(const KView& v, Cover& cv, const uint8_t* t, uint32_
   else if (f > cv.maxf || cv.maxf == kNone) cv.maxf = f;
 }
 
-__device__ int32_t eval_kafka(const KView& v, const KafkaHeader& h, const uint8_t* __restrict__ arena,
-                              uint64_t arena_bytes, uint64_t off, const uint32_t* crc_tab) {
-  if ((off & 3) || off + 4 > arena_bytes) return L7M_VERDICT_PARSE_ERROR;
-  const uint8_t* rec = arena + off;
+// One record whose first `limit` bytes are readable at rec (LDS stage or HBM).
+__device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader& h, const uint8_t* rec,
+                                              uint64_t limit, const uint32_t* crc_tab) {
+  if (limit < 4) return L7M_VERDICT_PARSE_ERROR;
   const int32_t msize = static_cast<int32_t>((static_cast<uint32_t>(rec[0]) << 24) |
                                              (static_cast<uint32_t>(rec[1]) << 16) |
                                              (static_cast<uint32_t>(rec[2]) << 8) | rec[3]);
   // ReadReq: size <= 0 / short kind read / allocParseBuf; ReadRequest: len < 12.
   if (msize < 8 || static_cast<int64_t>(msize) + 4 > kKafkaMaxParseBuf) return L7M_VERDICT_PARSE_ERROR;
-  if (off + 4 + static_cast<uint64_t>(msize) > arena_bytes) return L7M_VERDICT_PARSE_ERROR;
+  if (4 + static_cast<uint64_t>(msize) > limit) return L7M_VERDICT_PARSE_ERROR;
   const int32_t kind = static_cast<int16_t>((rec[4] << 8) | rec[5]);
   const int16_t version = static_cast<int16_t>((rec[6] << 8) | rec[7]);  // request.go:72-74
   const uint32_t kidx = (kind >= 0 && kind < 64) ? static_cast<uint32_t>(kind) : 64u;
@@ -419,15 +421,49 @@ __device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits
   }
 }
 
-template <bool kHits>
-__global__ __launch_bounds__(256) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
-                                                         const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                         const uint64_t* __restrict__ offs, uint64_t n,
-                                                         int32_t* __restrict__ verdicts,
-                                                         unsigned long long* __restrict__ hits) {
-  __shared__ uint32_t crc_tab[256];
+constexpr uint32_t kKWaves = 16;
+constexpr uint32_t kKBlock = 64 * kKWaves;
+constexpr uint32_t kKMaxStage = 8192;
+constexpr uint32_t kKCopyIters = kKMaxStage / 1024;
+constexpr uint32_t kKLdsBytes = 160 * 1024;
+constexpr uint32_t kKMaxLdsCounters = 16384;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
+  const uint32_t lo = __shfl(static_cast<uint32_t>(x), src);
+  const uint32_t hi = __shfl(static_cast<uint32_t>(x >> 32), src);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+enum KHitMode { kKNoHits = 0, kKLdsHits = 1, kKGlobalHits = 2 };
+
+// Persistent layout as the HTTP kernel: one 1024-thread workgroup per CU,
+// each wave consumes its contiguous share of the batch in tiles of <= 64
+// records copied HBM -> the wave's LDS stage (coalesced 16-byte loads, the
+// next tile's bytes in flight while this one is decoded); a record outside
+// its tile window is decoded from HBM.
+template <int kHits>
+__global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
+                                                             const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                             const uint64_t* __restrict__ offs, uint64_t n,
+                                                             int32_t* __restrict__ verdicts,
+                                                             unsigned long long* __restrict__ hits, uint32_t stage) {
+  extern __shared__ __align__(16) uint32_t ksmem[];
   const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) crc_tab[i] = prog[h.off_crc + i];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t n_ctr = h.n_rules + 2;
+  uint32_t* crc_tab = ksmem;
+  uint32_t* ctr = ksmem + 256;
+  uint8_t* stg = reinterpret_cast<uint8_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
+                 wv * (stage + 16u);
+  for (uint32_t i = tid; i < 256; i += kKBlock) crc_tab[i] = prog[h.off_crc + i];
+  if (kHits == kKLdsHits)
+    for (uint32_t i = tid; i < n_ctr; i += kKBlock) ctr[i] = 0;
   __syncthreads();
   KView v;
   v.prog = prog;
@@ -436,15 +472,118 @@ __global__ __launch_bounds__(256) void kafka_eval_kernel(const uint32_t* __restr
   v.pool = prog + h.off_pool;
   v.strings = reinterpret_cast<const uint8_t*>(prog + h.off_strings);
   v.n_slots = h.n_slots;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; r < n; r += stride) {
-    const int32_t verdict = eval_kafka(v, h, arena, arena_bytes, offs[r], crc_tab);
-    verdicts[r] = verdict;
-    if (kHits) {
-      const uint32_t slot = verdict >= 0 ? static_cast<uint32_t>(verdict) + 2 : (verdict == -1 ? 0u : 1u);
-      count_slot(hits, slot, true);
+
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kKWaves + wv;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kKWaves;
+  const uint64_t end = n * (gw + 1) / nw;
+  struct Tile {
+    uint64_t cur, o, onext, base;
+    uint32_t k, bytes, take;
+  };
+  auto load_offs = [&](uint64_t cur, uint64_t* o, uint64_t* onext) {
+    *o = 0;
+    *onext = 0;
+    if (cur < end && lane < end - cur) {
+      *o = offs[cur + lane];
+      *onext = cur + lane + 1 < n ? offs[cur + lane + 1] : arena_bytes;
     }
+  };
+  auto plan = [&](uint64_t cur, uint64_t o, uint64_t onext) -> Tile {
+    Tile t;
+    t.cur = cur;
+    t.o = o;
+    t.onext = onext;
+    if (cur >= end) {
+      t.base = 0;
+      t.k = t.bytes = t.take = 0;
+      return t;
+    }
+    const uint64_t m = end - cur < 64 ? end - cur : 64;
+    const uint64_t o0 = shfl64(o, 0);
+    t.base = o0 & ~15ull;
+    const bool ok = lane < m && (o & 3) == 0 && o >= o0 && onext >= o && onext <= arena_bytes &&
+                    onext - t.base <= stage;
+    const uint64_t okm = __ballot(ok);
+    t.k = okm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~okm));
+    t.bytes = t.k ? static_cast<uint32_t>(shfl64(onext, t.k - 1) - t.base) : 0u;
+    t.take = t.k ? t.k : 1u;
+    return t;
+  };
+  u32x4 buf[kKCopyIters];
+  auto issue_bytes = [&](const Tile& t) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
+#pragma unroll
+    for (uint32_t it = 0; it < kKCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
+    }
+  };
+  uint64_t o1, n1, o2, n2;
+  load_offs(n * gw / nw, &o1, &n1);
+  Tile t = plan(n * gw / nw, o1, n1);
+  issue_bytes(t);
+  load_offs(t.cur + t.take, &o2, &n2);
+  while (t.cur < end) {
+#pragma unroll
+    for (uint32_t it = 0; it < kKCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+    }
+    wave_sync();
+    const Tile t2 = plan(t.cur + t.take, o2, n2);
+    issue_bytes(t2);
+    load_offs(t2.cur + t2.take, &o2, &n2);
+
+    const uint64_t o = t.o, onext = t.onext;
+    int32_t verdict = 0;
+    if (lane < t.take) {
+      bool done = false;
+      if (lane < t.k && onext - o >= 4) {
+        const uint8_t* rec = stg + (o - t.base);
+        const uint32_t msize = (static_cast<uint32_t>(rec[0]) << 24) | (static_cast<uint32_t>(rec[1]) << 16) |
+                               (static_cast<uint32_t>(rec[2]) << 8) | rec[3];
+        if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
+          verdict = eval_kafka(v, h, rec, onext - o, crc_tab);
+          done = true;
+        }
+      }
+      if (!done) {  // outside the staged window: decode from HBM
+        const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
+        verdict = inb ? eval_kafka(v, h, arena + o, arena_bytes - o, crc_tab) : L7M_VERDICT_PARSE_ERROR;
+      }
+      verdicts[t.cur + lane] = verdict;
+    }
+    if (kHits != kKNoHits) {
+      uint32_t slot = kNone;
+      if (lane < t.take) slot = verdict >= 0 ? static_cast<uint32_t>(verdict) + 2 : (verdict == -1 ? 0u : 1u);
+      if (kHits == kKLdsHits) {
+        if (slot != kNone) atomicAdd(ctr + slot, 1u);
+      } else {
+        count_slot(hits, slot, slot != kNone);
+      }
+    }
+    wave_sync();  // the stage is overwritten by the next tile
+    t = t2;
   }
+  if (kHits == kKLdsHits) {
+    __syncthreads();
+    for (uint32_t i = tid; i < n_ctr; i += kKBlock)
+      if (ctr[i]) atomicAdd(hits + i, static_cast<unsigned long long>(ctr[i]));
+  }
+}
+
+template <int kHits>
+static void launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
+                     uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
+                     unsigned long long* hits, uint32_t stage) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kafka_eval_kernel<kHits>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kKLdsBytes);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((kafka_eval_kernel<kHits>), grid, dim3(kKBlock), lds, stream, dprog, arena, arena_bytes, offs,
+                     n, verdicts, hits, stage);
 }
 
 }  // namespace
@@ -452,18 +591,22 @@ __global__ __launch_bounds__(256) void kafka_eval_kernel(const uint32_t* __restr
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                         const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
                         hipStream_t stream, int num_cus) {
-  (void)h;
   if (n == 0) return hipSuccess;
-  const uint32_t block = 256;
-  uint64_t blocks = (n + block - 1) / block;
-  const uint64_t cap = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * 8;
-  if (blocks > cap) blocks = cap;
-  if (hits)
-    hipLaunchKernelGGL(kafka_eval_kernel<true>, dim3(static_cast<uint32_t>(blocks)), dim3(block), 0, stream, dprog,
-                       arena, arena_bytes, offs, n, verdicts, hits);
-  else
-    hipLaunchKernelGGL(kafka_eval_kernel<false>, dim3(static_cast<uint32_t>(blocks)), dim3(block), 0, stream, dprog,
-                       arena, arena_bytes, offs, n, verdicts, hits);
+  const uint32_t n_ctr = h.n_rules + 2;
+  const int mode = !hits ? kKNoHits : (n_ctr <= kKMaxLdsCounters ? kKLdsHits : kKGlobalHits);
+  const size_t fixed = 4u * (256u + (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
+  size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
+  stage &= ~size_t(15);
+  if (stage > kKMaxStage) stage = kKMaxStage;
+  const size_t lds = fixed + kKWaves * (stage + 16u);
+  uint64_t blocks = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256);
+  const uint64_t want = (n + 8 * kKBlock - 1) / (8 * kKBlock);
+  if (want < blocks) blocks = want;
+  const dim3 grid(static_cast<uint32_t>(blocks));
+  const uint32_t st = static_cast<uint32_t>(stage);
+  if (mode == kKNoHits) launch_k<kKNoHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
+  else if (mode == kKLdsHits) launch_k<kKLdsHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
+  else launch_k<kKGlobalHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
   return hipGetLastError();
 }
 
