@@ -11,7 +11,8 @@
 //     them, and those with Topic == "";
 //   * an open-addressed table Topic -> ascending ids of the rules with that
 //     Topic (the reqTopicsMap coverage walk of policy.go:210-223);
-//   * per rule: apiKeyInt mask, apiVersionInt, ClientID (hash + bytes).
+//   * per rule: apiKeyInt mask, apiVersionInt, interned ClientID; a table
+//     ClientID -> index resolves a request's ClientID once.
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -193,10 +194,12 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   };
   std::vector<KafkaRuleDesc> desc(n);
   std::map<std::string, std::vector<uint32_t>> by_topic;
+  std::map<std::string, uint32_t> client_ids;
   for (size_t i = 0; i < n; ++i) {
     const KRule& r = kr[i];
     KafkaRuleDesc& d = desc[i];
     std::memset(&d, 0, sizeof d);
+    d.client_idx = kNone;
     if (r.keys.empty()) d.flags |= kKRuleAnyKey;
     for (int k : r.keys) {
       if (k < 32) d.keys_lo |= 1u << k;
@@ -208,9 +211,8 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
     }
     if (!r.client.empty()) {
       d.flags |= kKRuleClient;
-      d.client_hash = fnv1a(r.client);
-      d.client_off = put_str(r.client);
-      d.client_len = static_cast<uint32_t>(r.client.size());
+      auto it = client_ids.emplace(r.client, static_cast<uint32_t>(client_ids.size())).first;
+      d.client_idx = it->second;
     }
     if (!r.topic.empty()) {
       d.flags |= kKRuleTopic;
@@ -240,22 +242,49 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
     h.notopic_by_kind[k] = push_list(notopic);
   }
 
-  // topic table (load factor <= 1/2)
-  uint32_t n_slots = 0;
-  if (!by_topic.empty()) {
-    n_slots = 2;
-    while (n_slots < 2 * by_topic.size()) n_slots <<= 1;
-  }
+  auto table_size = [](size_t keys) -> uint32_t {  // load factor <= 1/2
+    if (!keys) return 0;
+    uint32_t m = 2;
+    while (m < 2 * keys) m <<= 1;
+    return m;
+  };
+  auto put_prefix = [](uint32_t* pfx, size_t cap, const std::string& s) {
+    std::memcpy(pfx, s.data(), std::min(cap, s.size()));
+  };
+  const uint32_t n_slots = table_size(by_topic.size());
   std::vector<KafkaTopicSlot> slots(n_slots);
   std::memset(slots.data(), 0, slots.size() * sizeof(KafkaTopicSlot));
   for (const auto& kv : by_topic) {
     uint32_t hk = kafka_key_hash(fnv1a(kv.first));
     uint32_t at = hk & (n_slots - 1);
     while (slots[at].hash != 0) at = (at + 1) & (n_slots - 1);
-    slots[at].hash = hk;
-    slots[at].str_off = put_str(kv.first);
-    slots[at].str_len = static_cast<uint32_t>(kv.first.size());
-    slots[at].rules = push_list(kv.second);
+    KafkaTopicSlot& sl = slots[at];
+    sl.hash = hk;
+    sl.str_off = put_str(kv.first);
+    sl.str_len = static_cast<uint32_t>(kv.first.size());
+    sl.rules = push_list(kv.second);
+    const KafkaRuleDesc& d = desc[kv.second[0]];
+    sl.r0_id = kv.second[0];
+    sl.r0_flags = d.flags | (static_cast<uint32_t>(static_cast<uint16_t>(d.version)) << 16);
+    sl.r0_keys_lo = d.keys_lo;
+    sl.r0_keys_hi = d.keys_hi;
+    sl.r0_client = d.client_idx;
+    put_prefix(sl.pfx, kTopicInline, kv.first);
+  }
+
+  const uint32_t n_clients = table_size(client_ids.size());
+  std::vector<KafkaClientSlot> cslots(n_clients);
+  std::memset(cslots.data(), 0, cslots.size() * sizeof(KafkaClientSlot));
+  for (const auto& kv : client_ids) {
+    uint32_t hk = kafka_key_hash(fnv1a(kv.first));
+    uint32_t at = hk & (n_clients - 1);
+    while (cslots[at].hash != 0) at = (at + 1) & (n_clients - 1);
+    KafkaClientSlot& sl = cslots[at];
+    sl.hash = hk;
+    sl.str_off = put_str(kv.first);
+    sl.str_len = static_cast<uint32_t>(kv.first.size());
+    sl.idx = kv.second;
+    put_prefix(sl.pfx, kClientInline, kv.first);
   }
 
   uint32_t crc[256];
@@ -266,7 +295,8 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   }
 
   uint64_t w = sizeof(KafkaHeader) / 4;
-  auto take = [&](uint64_t words) {
+  auto take = [&](uint64_t words) {  // 16-byte aligned sections
+    w = (w + 3) & ~uint64_t(3);
     uint64_t o = w;
     w += words;
     return static_cast<uint32_t>(o);
@@ -274,6 +304,8 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   h.off_rules = take(static_cast<uint64_t>(n) * sizeof(KafkaRuleDesc) / 4);
   h.off_slots = take(static_cast<uint64_t>(n_slots) * sizeof(KafkaTopicSlot) / 4);
   h.n_slots = n_slots;
+  h.off_clients = take(static_cast<uint64_t>(n_clients) * sizeof(KafkaClientSlot) / 4);
+  h.n_clients = n_clients;
   h.off_pool = take(pool.size());
   h.off_crc = take(256);
   h.off_strings = take((strings.size() + 3) / 4);
@@ -284,6 +316,8 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   std::memcpy(prog.data(), &h, sizeof h);
   if (n) std::memcpy(prog.data() + h.off_rules, desc.data(), n * sizeof(KafkaRuleDesc));
   if (n_slots) std::memcpy(prog.data() + h.off_slots, slots.data(), n_slots * sizeof(KafkaTopicSlot));
+  if (n_clients)
+    std::memcpy(prog.data() + h.off_clients, cslots.data(), n_clients * sizeof(KafkaClientSlot));
   if (!pool.empty()) std::memcpy(prog.data() + h.off_pool, pool.data(), pool.size() * 4);
   std::memcpy(prog.data() + h.off_crc, crc, sizeof crc);
   if (!strings.empty()) std::memcpy(prog.data() + h.off_strings, strings.data(), strings.size());

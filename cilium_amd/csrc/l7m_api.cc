@@ -96,7 +96,7 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
     std::memcpy(&h, rs->program.data(), sizeof h);
     e = launch_kafka(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
                      n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
-                     stream, cus);
+                     stream, cus, flags);
   } else {
     return L7M_EINVAL;
   }

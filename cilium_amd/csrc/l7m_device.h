@@ -19,6 +19,6 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
 
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena,
                         uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                        unsigned long long* hits, hipStream_t stream, int num_cus);
+                        unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags);
 
 }  // namespace l7m

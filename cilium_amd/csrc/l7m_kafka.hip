@@ -150,89 +150,109 @@ struct KView {
   const uint32_t* prog;
   const KafkaRuleDesc* rules;
   const KafkaTopicSlot* slots;
+  const KafkaClientSlot* clients;
   const uint32_t* pool;
   const uint8_t* strings;
-  uint32_t n_slots;
+  uint32_t n_slots, n_clients;
 };
 
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i)
-    if (a[i] != b[i]) return false;
+// s[0..len) == the table string whose first kInl bytes are inline in pfx
+// (zero padded) and whose whole text is at rest.
+template <uint32_t kInl>
+__device__ __forceinline__ bool str_eq(const uint8_t* s, uint32_t len, const uint32_t (&pfx)[kInl / 4],
+                                       const uint8_t* rest) {
+#pragma unroll
+  for (uint32_t w = 0; w < kInl / 4; ++w) {
+    if (4 * w >= len) break;
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+      if (4 * w + k < len) x |= static_cast<uint32_t>(s[4 * w + k]) << (8 * k);
+    if (x != pfx[w]) return false;
+  }
+  for (uint32_t i = kInl; i < len; ++i)
+    if (s[i] != rest[i]) return false;
   return true;
 }
 
 // ruleMatches (policy.go:144-195) minus CheckAPIKeyRole, which list
 // membership already guarantees: version, then the ClientID condition when
-// `check_client` (typed requests with a Topic/ClientID-bearing rule).
-__device__ __forceinline__ bool rule_rest_ok(const KView& v, uint32_t rid, int16_t version, bool check_client,
-                                             const uint8_t* client, uint32_t client_len, uint32_t client_hash) {
-  const KafkaRuleDesc r = v.rules[rid];
-  if ((r.flags & kKRuleVersion) && r.version != version) return false;
-  if (check_client && (r.flags & kKRuleClient)) {
-    if (r.client_len != client_len || r.client_hash != client_hash) return false;
-    if (!bytes_eq(v.strings + r.client_off, client, client_len)) return false;
-  }
+// `check_client` (typed requests).  client = the request's interned ClientID
+// (kNone when no rule names it).
+__device__ __forceinline__ bool rest_ok(uint32_t flags, int32_t rversion, uint32_t rclient, int16_t version,
+                                        bool check_client, uint32_t client) {
+  if ((flags & kKRuleVersion) && rversion != version) return false;
+  if (check_client && (flags & kKRuleClient) && rclient != client) return false;
   return true;
 }
 
-__device__ __forceinline__ bool key_ok(const KafkaRuleDesc& r, int32_t kind) {
-  if (r.flags & kKRuleAnyKey) return true;
+__device__ __forceinline__ bool key_ok(uint32_t flags, uint32_t keys_lo, uint32_t keys_hi, int32_t kind) {
+  if (flags & kKRuleAnyKey) return true;
   if (kind < 0 || kind >= 64) return false;
-  return kind < 32 ? ((r.keys_lo >> kind) & 1u) : ((r.keys_hi >> (kind - 32)) & 1u);
+  return kind < 32 ? ((keys_lo >> kind) & 1u) : ((keys_hi >> (kind - 32)) & 1u);
 }
 
-// First rule of an ascending candidate list (ids < limit) passing rule_rest_ok.
-__device__ uint32_t first_in(const KView& v, Span s, uint32_t limit, int16_t version, bool check_client,
-                             const uint8_t* client, uint32_t client_len, uint32_t client_hash) {
-  for (uint32_t j = 0; j < s.len; ++j) {
+// First rule of an ascending candidate list (ids < limit) passing rest_ok.
+__device__ uint32_t first_in(const KView& v, Span s, uint32_t skip, uint32_t limit, int32_t kind, bool need_key,
+                             int16_t version, bool check_client, uint32_t client) {
+  for (uint32_t j = skip; j < s.len; ++j) {
     const uint32_t rid = v.pool[s.off + j];
     if (rid >= limit) break;
-    if (rule_rest_ok(v, rid, version, check_client, client, client_len, client_hash)) return rid;
+    const KafkaRuleDesc r = v.rules[rid];
+    if ((!need_key || key_ok(r.flags, r.keys_lo, r.keys_hi, kind)) &&
+        rest_ok(r.flags, r.version, r.client_idx, version, check_client, client))
+      return rid;
   }
   return kNone;
 }
 
-// Per-request coverage state of the topic walk (policy.go:210-223).
-struct Cover {
-  uint32_t j;      // first Topic=="" rule with ruleMatches (kNone if none)
-  uint32_t maxf;   // max over topics of the first covering rule
-  bool ok;         // every topic so far has a covering rule below j
-};
-
-__device__ void cover_topic(const KView& v, Cover& cv, const uint8_t* t, uint32_t tlen, int32_t kind,
-                            int16_t version, const uint8_t* client, uint32_t client_len,
-                            uint32_t client_hash) {
-  if (!cv.ok) return;
-  uint32_t f = kNone;
-  if (tlen && v.n_slots) {
-    uint32_t h = kFnvBasis;
-    for (uint32_t i = 0; i < tlen; ++i) h = fnv1a_step(h, t[i]);
-    h = kafka_key_hash(h);
-    for (uint32_t at = h & (v.n_slots - 1);; at = (at + 1) & (v.n_slots - 1)) {
-      const KafkaTopicSlot sl = v.slots[at];
-      if (sl.hash == 0) break;
-      if (sl.hash == h && sl.str_len == tlen && bytes_eq(v.strings + sl.str_off, t, tlen)) {
-        for (uint32_t j = 0; j < sl.rules.len; ++j) {
-          const uint32_t rid = v.pool[sl.rules.off + j];
-          if (rid >= cv.j) break;
-          if (key_ok(v.rules[rid], kind) &&
-              rule_rest_ok(v, rid, version, true, client, client_len, client_hash)) {
-            f = rid;
-            break;
-          }
-        }
-        break;
-      }
-    }
+// The request ClientID's index among the rules' ClientIDs (kNone if none).
+__device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t* c, uint32_t len, uint32_t hash) {
+  if (!len || !v.n_clients) return kNone;
+  const uint32_t hk = kafka_key_hash(hash);
+  for (uint32_t at = hk & (v.n_clients - 1);; at = (at + 1) & (v.n_clients - 1)) {
+    const KafkaClientSlot sl = v.clients[at];
+    if (sl.hash == 0) return kNone;
+    if (sl.hash == hk && sl.str_len == len && str_eq<kClientInline>(c, len, sl.pfx, v.strings + sl.str_off))
+      return sl.idx;
   }
-  // A topic without a covering rule below j leaves min(j, .) = j.
-  if (f == kNone) cv.ok = false;
-  else if (f > cv.maxf || cv.maxf == kNone) cv.maxf = f;
 }
 
+// First rule whose Topic is t[0..tlen) and whose CheckAPIKeyRole / version /
+// ClientID conditions hold (kNone if none): the per-topic term of the
+// reqTopicsMap coverage walk (policy.go:210-223).
+__device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t, uint32_t tlen, int32_t kind,
+                                                int16_t version, uint32_t client) {
+  if (!tlen || !v.n_slots) return kNone;
+  uint32_t h = kFnvBasis;
+  for (uint32_t i = 0; i < tlen; ++i) h = fnv1a_step(h, t[i]);
+  h = kafka_key_hash(h);
+  for (uint32_t at = h & (v.n_slots - 1);; at = (at + 1) & (v.n_slots - 1)) {
+    const KafkaTopicSlot sl = v.slots[at];
+    if (sl.hash == 0) return kNone;
+    if (sl.hash == h && sl.str_len == tlen && str_eq<kTopicInline>(t, tlen, sl.pfx, v.strings + sl.str_off)) {
+      if (key_ok(sl.r0_flags, sl.r0_keys_lo, sl.r0_keys_hi, kind) &&
+          rest_ok(sl.r0_flags, static_cast<int16_t>(sl.r0_flags >> 16), sl.r0_client, version, true, client))
+        return sl.r0_id;
+      return sl.rules.len > 1 ? first_in(v, sl.rules, 1, kNone, kind, true, version, true, client) : kNone;
+    }
+  }
+}
+
+// Topics are resolved after the decode, all lanes of the wave together
+// (the decode itself diverges by request kind): each lane parks the offsets
+// of its first kTopicQ topic names in its LDS column and the lookups run in
+// lock-step rounds.  Because MatchesRule's result is
+//   min(j, max over topics of f(t))   (f(t) = topic_first, kNone = uncovered)
+// with j the first Topic=="" rule, the per-topic terms need neither j nor
+// any order, so a lane whose request has more topics resolves the excess
+// ones during the decode.
+constexpr uint32_t kTopicQ = 4;
+
 // One record whose first `limit` bytes are readable at rec (LDS stage or HBM).
+// tq: this lane's topic column (kTopicQ entries, stride 64 words) in LDS.
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader& h, const uint8_t* rec,
-                                              uint64_t limit, const uint32_t* crc_tab) {
+                                              uint64_t limit, const uint32_t* crc_tab, uint32_t* tq) {
   if (limit < 4) return L7M_VERDICT_PARSE_ERROR;
   const int32_t msize = static_cast<int32_t>((static_cast<uint32_t>(rec[0]) << 24) |
                                              (static_cast<uint32_t>(rec[1]) << 16) |
@@ -249,8 +269,8 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader&
   if (!typed) {
     // request == nil: matchNonTopicRequests (policy.go:54-70), ClientID ignored.
     const bool topic_kind = kind >= 0 && kind < 64 && ((kTopicApiKeyMask >> kind) & 1ull);
-    first = first_in(v, topic_kind ? h.notopic_by_kind[kidx] : h.all_by_kind[kidx], kNone, version, false,
-                     nullptr, 0, 0);
+    first = first_in(v, topic_kind ? h.notopic_by_kind[kidx] : h.all_by_kind[kidx], 0, kNone, kind, false,
+                     version, false, kNone);
   } else {
     Rd d{rec, 4u + static_cast<uint32_t>(msize), 12, false};
     uint32_t coff, clen;
@@ -258,23 +278,26 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader&
     const uint8_t* client = rec + coff;
     uint32_t chash = kFnvBasis;
     for (uint32_t i = 0; i < clen; ++i) chash = fnv1a_step(chash, client[i]);
+    const uint32_t cid = intern_client(v, client, clen, chash);
 
     int32_t ntop = 0;
     bool ok = true;
     int ms = kMsOk;
-    Cover cv{kNone, kNone, true};
-    // Called after the topic array length is known: j (the Topic=="" rules)
-    // is needed only when there are topics.
-    auto start_topics = [&](int32_t n) {
-      ntop = n;
-      if (n > 0 && kind != 10) {
-        cv.j = first_in(v, h.notopic_by_kind[kidx], kNone, version, true, client, clen, chash);
-      }
-    };
+    uint32_t maxf = 0, nq = 0;
+    auto start_topics = [&](int32_t n) { ntop = n; };
     auto topic = [&]() {
       uint32_t toff, tlen;
       rd_str(d, &toff, &tlen);
-      if (!d.err) cover_topic(v, cv, rec + toff, tlen, kind, version, client, clen, chash);
+      if (d.err || maxf == kNone) return;
+      if (!tlen) {
+        maxf = kNone;
+      } else if (nq < kTopicQ) {
+        tq[64 * nq] = toff;
+        ++nq;
+      } else {
+        const uint32_t f = topic_first(v, rec + toff, tlen, kind, version, cid);
+        maxf = f > maxf ? f : maxf;
+      }
     };
     int32_t n, np;
     switch (kind) {
@@ -398,12 +421,18 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader&
     if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
     if (kind == 10) {
       // ConsumerMetadataReq: GetTopics() is nil and ruleMatches -> true.
-      first = first_in(v, h.all_by_kind[kidx], kNone, version, false, nullptr, 0, 0);
+      first = first_in(v, h.all_by_kind[kidx], 0, kNone, kind, false, version, false, kNone);
     } else if (ntop == 0) {
-      first = first_in(v, h.all_by_kind[kidx], kNone, version, true, client, clen, chash);
+      first = first_in(v, h.all_by_kind[kidx], 0, kNone, kind, false, version, true, cid);
     } else {
-      first = cv.ok ? cv.maxf : cv.j;
-      if (cv.j < first) first = cv.j;
+      for (uint32_t r = 0; r < nq && maxf != kNone; ++r) {
+        const uint32_t toff = tq[64 * r];
+        const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
+        const uint32_t f = topic_first(v, rec + toff, tlen, kind, version, cid);
+        maxf = f > maxf ? f : maxf;
+      }
+      const uint32_t j = first_in(v, h.notopic_by_kind[kidx], 0, maxf, kind, false, version, true, cid);
+      first = j < maxf ? j : maxf;
     }
   }
   return first == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(first);
@@ -447,7 +476,9 @@ enum KHitMode { kKNoHits = 0, kKLdsHits = 1, kKGlobalHits = 2 };
 // records copied HBM -> the wave's LDS stage (coalesced 16-byte loads, the
 // next tile's bytes in flight while this one is decoded); a record outside
 // its tile window is decoded from HBM.
-template <int kHits>
+// kAblate (diagnostics only, L7M_FLAG_DIAG_*): 1 = stage records, no
+// decoding; 2 = decode without table lookups.
+template <int kHits, int kAblate>
 __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
                                                              const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                              const uint64_t* __restrict__ offs, uint64_t n,
@@ -459,8 +490,9 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   const uint32_t n_ctr = h.n_rules + 2;
   uint32_t* crc_tab = ksmem;
   uint32_t* ctr = ksmem + 256;
-  uint8_t* stg = reinterpret_cast<uint8_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
-                 wv * (stage + 16u);
+  uint32_t* tq = ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);
+  uint8_t* stg = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ) + wv * (stage + 16u);
+  tq += wv * 64 * kTopicQ + lane;
   for (uint32_t i = tid; i < 256; i += kKBlock) crc_tab[i] = prog[h.off_crc + i];
   if (kHits == kKLdsHits)
     for (uint32_t i = tid; i < n_ctr; i += kKBlock) ctr[i] = 0;
@@ -469,9 +501,11 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   v.prog = prog;
   v.rules = reinterpret_cast<const KafkaRuleDesc*>(prog + h.off_rules);
   v.slots = reinterpret_cast<const KafkaTopicSlot*>(prog + h.off_slots);
+  v.clients = reinterpret_cast<const KafkaClientSlot*>(prog + h.off_clients);
+  v.n_clients = kAblate == 2 ? 0 : h.n_clients;
   v.pool = prog + h.off_pool;
   v.strings = reinterpret_cast<const uint8_t*>(prog + h.off_strings);
-  v.n_slots = h.n_slots;
+  v.n_slots = kAblate == 2 ? 0 : h.n_slots;
 
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kKWaves + wv;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kKWaves;
@@ -542,14 +576,17 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
         const uint8_t* rec = stg + (o - t.base);
         const uint32_t msize = (static_cast<uint32_t>(rec[0]) << 24) | (static_cast<uint32_t>(rec[1]) << 16) |
                                (static_cast<uint32_t>(rec[2]) << 8) | rec[3];
-        if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka(v, h, rec, onext - o, crc_tab);
+        if (kAblate == 1) {
+          verdict = static_cast<int32_t>(msize & 1u) - 1;
+          done = true;
+        } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
+          verdict = eval_kafka(v, h, rec, onext - o, crc_tab, tq);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka(v, h, arena + o, arena_bytes - o, crc_tab) : L7M_VERDICT_PARSE_ERROR;
+        verdict = inb ? eval_kafka(v, h, arena + o, arena_bytes - o, crc_tab, tq) : L7M_VERDICT_PARSE_ERROR;
       }
       verdicts[t.cur + lane] = verdict;
     }
@@ -572,17 +609,17 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   }
 }
 
-template <int kHits>
+template <int kHits, int kAblate = 0>
 static void launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                      uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                      unsigned long long* hits, uint32_t stage) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kafka_eval_kernel<kHits>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kKLdsBytes);
     attr_set = true;
   }
-  hipLaunchKernelGGL((kafka_eval_kernel<kHits>), grid, dim3(kKBlock), lds, stream, dprog, arena, arena_bytes, offs,
+  hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate>), grid, dim3(kKBlock), lds, stream, dprog, arena, arena_bytes, offs,
                      n, verdicts, hits, stage);
 }
 
@@ -590,11 +627,11 @@ static void launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* 
 
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                         const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
-                        hipStream_t stream, int num_cus) {
+                        hipStream_t stream, int num_cus, uint32_t flags) {
   if (n == 0) return hipSuccess;
   const uint32_t n_ctr = h.n_rules + 2;
   const int mode = !hits ? kKNoHits : (n_ctr <= kKMaxLdsCounters ? kKLdsHits : kKGlobalHits);
-  const size_t fixed = 4u * (256u + (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
+  const size_t fixed = 4u * (256u + (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u) + kKWaves * 64 * kTopicQ);
   size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
   stage &= ~size_t(15);
   if (stage > kKMaxStage) stage = kKMaxStage;
@@ -604,6 +641,13 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   if (want < blocks) blocks = want;
   const dim3 grid(static_cast<uint32_t>(blocks));
   const uint32_t st = static_cast<uint32_t>(stage);
+  if (flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) {
+    if (flags & L7M_FLAG_DIAG_COPY_ONLY)
+      launch_k<kKNoHits, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
+    else
+      launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
+    return hipGetLastError();
+  }
   if (mode == kKNoHits) launch_k<kKNoHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
   else if (mode == kKLdsHits) launch_k<kKLdsHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
   else launch_k<kKGlobalHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);

@@ -127,24 +127,42 @@ static_assert(sizeof(HttpHeader) == 128, "header is 32 words");
 // Rule semantics follow pkg/kafka/policy.go:144-225 and
 // pkg/policy/api/kafka.go:248-271 (after Sanitize, rule_validation.go:190-233).
 struct KafkaRuleDesc {
-  uint32_t flags;        // kKRule* bits
-  int32_t version;       // apiVersionInt when kKRuleVersion
-  uint32_t keys_lo;      // apiKeyInt as a bitmask over kinds 0..63 (unless kKRuleAnyKey)
+  uint32_t flags;       // kKRule* bits
+  int32_t version;      // apiVersionInt when kKRuleVersion
+  uint32_t keys_lo;     // apiKeyInt as a bitmask over kinds 0..63 (unless kKRuleAnyKey)
   uint32_t keys_hi;
-  uint32_t client_hash;  // fnv1a32(ClientID) when kKRuleClient
-  uint32_t client_off;   // byte offset of ClientID in the string area
-  uint32_t client_len;
-  uint32_t pad;
+  uint32_t client_idx;  // interned ClientID when kKRuleClient (KafkaClientSlot::idx)
+  uint32_t pad[3];
 };
 constexpr uint32_t kKRuleAnyKey = 1u, kKRuleVersion = 2u, kKRuleTopic = 4u, kKRuleClient = 8u;
 
 // Open-addressed (linear probing) table: Topic -> ascending ids of the rules
 // whose Topic equals it.  hash == 0 marks an empty slot (see kafka_key_hash).
+// One 64-byte slot carries the first rule's check fields and the first
+// kTopicInline bytes of the topic (zero padded), so the common case (one
+// rule per topic, short names) resolves with a single slot fetch.
+constexpr uint32_t kTopicInline = 24;
 struct KafkaTopicSlot {
   uint32_t hash;
-  uint32_t str_off, str_len;  // bytes in the string area
-  Span rules;                 // into the u32 pool
-  uint32_t pad[3];
+  uint32_t str_len;
+  uint32_t str_off;      // whole topic in the string area
+  Span rules;            // ascending rule ids in the u32 pool
+  uint32_t r0_id;        // == pool[rules.off]
+  uint32_t r0_flags;     // flags | (uint16)version << 16
+  uint32_t r0_keys_lo, r0_keys_hi;
+  uint32_t r0_client;    // client_idx
+  uint32_t pfx[kTopicInline / 4];
+};
+
+// Interned rule ClientIDs: one lookup per request turns its ClientID into
+// the index a rule's client_idx is compared with.
+constexpr uint32_t kClientInline = 16;
+struct KafkaClientSlot {
+  uint32_t hash;
+  uint32_t str_len;
+  uint32_t str_off;
+  uint32_t idx;
+  uint32_t pfx[kClientInline / 4];
 };
 
 constexpr uint32_t kKafkaKinds = 65;  // request kinds 0..63; [64] = any other value
@@ -159,13 +177,17 @@ struct KafkaHeader {
   uint32_t off_crc;      // u32[256] CRC-32 (IEEE) table for message-set CRCs
   uint32_t off_strings;  // byte area (word offset)
   uint32_t total_words;
-  uint32_t pad[7];
+  uint32_t off_clients;  // KafkaClientSlot[n_clients]
+  uint32_t n_clients;    // power of two (0 when no rule has a ClientID)
+  uint32_t pad[5];
   // Ascending ids of the rules whose CheckAPIKeyRole(kind) holds:
   Span notopic_by_kind[kKafkaKinds];  // ... and Topic == ""
   Span all_by_kind[kKafkaKinds];      // ... any Topic
 };
 static_assert(sizeof(KafkaRuleDesc) == 32, "rule desc is 8 words");
-static_assert(sizeof(KafkaTopicSlot) == 32, "slot is 8 words");
+static_assert(sizeof(KafkaTopicSlot) == 64, "topic slot is 16 words");
+static_assert(sizeof(KafkaClientSlot) == 32, "client slot is 8 words");
+static_assert(sizeof(KafkaHeader) % 16 == 0, "header is whole 16-byte lines");
 
 constexpr uint32_t kFnvBasis = 2166136261u;
 __host__ __device__ inline uint32_t fnv1a_step(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }

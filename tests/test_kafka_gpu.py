@@ -124,3 +124,33 @@ def test_eval_device_and_shard_invariance(gpu):
     a1, o1 = W.requests(3, 0, 100_000)
     a2, o2 = W.requests(3, 100_000, 100_000)
     assert (np.concatenate([rs.eval(a1, o1), rs.eval(a2, o2)]) == host_v).all()
+
+
+def test_long_and_prefix_sharing_names_parity(gpu):
+    """Topic / ClientID names longer than the inline prefixes of the topic and
+    client tables (24 / 16 bytes) and names equal up to and past them."""
+    rng = np.random.default_rng(11)
+    stem = "orders.eu-west-1.payments.settlement"
+    topics = [stem[:k] for k in (1, 4, 23, 24, 25, 28, 36)] + [stem + "-%d" % i for i in range(5)]
+    topics += [stem[:24] + "X", stem[:25] + "Y"]
+    clients = ["svc-client-%s" % ("x" * k) for k in (0, 4, 5, 6, 12)] + ["c"]
+    rules = _random_rules(rng, 60, topics[:-3], clients[:-1])
+    # several rules per topic with failing first candidates
+    rules += [L.PortRuleKafka(APIKey="fetch", APIVersion="9", Topic=t) for t in topics[:4]]
+    rules += [L.PortRuleKafka(ClientID=clients[2], Topic=t) for t in topics[:6]]
+    recs = K.random_requests(rng, 6000, topics + ["zz"], clients + [clients[3] + "z", ""])
+    arena, offs = L.pack_records(recs)
+    _check(rules, arena, offs, hits=True)
+
+
+def test_many_rules_global_counters_parity(gpu):
+    """More rules than the kernel's LDS counter array holds (global hit
+    counting path)."""
+    rng = np.random.default_rng(13)
+    topics = ["topic-%d" % i for i in range(9000)]
+    rules = [L.PortRuleKafka(APIKey=str(rng.choice(["produce", "fetch", "metadata"])),
+                             ClientID="client-%d" % (i % 50) if i % 3 == 0 else "", Topic=topics[i % 9000])
+             for i in range(20000)]
+    recs = K.random_requests(rng, 20000, topics[:3000] + ["nope"], ["client-%d" % i for i in range(60)])
+    arena, offs = L.pack_records(recs)
+    _check(rules, arena, offs, hits=True)
