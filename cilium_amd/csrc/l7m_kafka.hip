@@ -156,22 +156,49 @@ struct KView {
   uint32_t n_slots, n_clients;
 };
 
-// s[0..len) == the table string whose first kInl bytes are inline in pfx
-// (zero padded) and whose whole text is at rest.
-template <uint32_t kInl>
-__device__ __forceinline__ bool str_eq(const uint8_t* s, uint32_t len, const uint32_t (&pfx)[kInl / 4],
-                                       const uint8_t* rest) {
+// The first 24 bytes of the name t[0..len) as little-endian words, zero
+// past len, from aligned dword reads of the words that hold name bytes
+// (records are dword aligned in both the LDS stage and the arena).
+constexpr uint32_t kNameWords = 6;
+struct Name {
+  uint32_t x[kNameWords];
+  uint32_t hash;  // FNV-1a 32 of the whole name
+};
+
+__device__ __forceinline__ Name load_name(const uint8_t* t, uint32_t len) {
+  Name nm;
+  const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(t)) & 3u;
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(t - sh);
+  uint32_t w[kNameWords + 1];
 #pragma unroll
-  for (uint32_t w = 0; w < kInl / 4; ++w) {
-    if (4 * w >= len) break;
-    uint32_t x = 0;
+  for (uint32_t k = 0; k <= kNameWords; ++k) w[k] = 4 * k < sh + len ? a[k] : 0u;
+  uint32_t h = kFnvBasis;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-      if (4 * w + k < len) x |= static_cast<uint32_t>(s[4 * w + k]) << (8 * k);
-    if (x != pfx[w]) return false;
+  for (uint32_t k = 0; k < kNameWords; ++k) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
+    nm.x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b)
+      if (static_cast<int32_t>(b) < rem) h = fnv1a_step(h, (nm.x[k] >> (8 * b)) & 0xffu);
   }
+  for (uint32_t i = 4 * kNameWords; i < len; ++i) h = fnv1a_step(h, t[i]);
+  nm.hash = h;
+  return nm;
+}
+
+// t[0..len) (loaded as nm) == the table string whose first kInl bytes are
+// inline in pfx (zero padded) and whose whole text is at rest.
+template <uint32_t kInl>
+__device__ __forceinline__ bool str_eq(const Name& nm, const uint8_t* t, uint32_t len,
+                                       const uint32_t (&pfx)[kInl / 4], const uint8_t* rest) {
+  static_assert(kInl <= 4 * kNameWords, "inline prefix longer than the loaded name");
+  bool eq = true;
+#pragma unroll
+  for (uint32_t k = 0; k < kInl / 4; ++k) eq &= nm.x[k] == pfx[k];
+  if (!eq) return false;
   for (uint32_t i = kInl; i < len; ++i)
-    if (s[i] != rest[i]) return false;
+    if (t[i] != rest[i]) return false;
   return true;
 }
 
@@ -207,13 +234,14 @@ __device__ uint32_t first_in(const KView& v, Span s, uint32_t skip, uint32_t lim
 }
 
 // The request ClientID's index among the rules' ClientIDs (kNone if none).
-__device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t* c, uint32_t len, uint32_t hash) {
+__device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t* c, uint32_t len) {
   if (!len || !v.n_clients) return kNone;
-  const uint32_t hk = kafka_key_hash(hash);
+  const Name nm = load_name(c, len);
+  const uint32_t hk = kafka_key_hash(nm.hash);
   for (uint32_t at = hk & (v.n_clients - 1);; at = (at + 1) & (v.n_clients - 1)) {
     const KafkaClientSlot sl = v.clients[at];
     if (sl.hash == 0) return kNone;
-    if (sl.hash == hk && sl.str_len == len && str_eq<kClientInline>(c, len, sl.pfx, v.strings + sl.str_off))
+    if (sl.hash == hk && sl.str_len == len && str_eq<kClientInline>(nm, c, len, sl.pfx, v.strings + sl.str_off))
       return sl.idx;
   }
 }
@@ -224,13 +252,12 @@ __device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t*
 __device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t, uint32_t tlen, int32_t kind,
                                                 int16_t version, uint32_t client) {
   if (!tlen || !v.n_slots) return kNone;
-  uint32_t h = kFnvBasis;
-  for (uint32_t i = 0; i < tlen; ++i) h = fnv1a_step(h, t[i]);
-  h = kafka_key_hash(h);
+  const Name nm = load_name(t, tlen);
+  const uint32_t h = kafka_key_hash(nm.hash);
   for (uint32_t at = h & (v.n_slots - 1);; at = (at + 1) & (v.n_slots - 1)) {
     const KafkaTopicSlot sl = v.slots[at];
     if (sl.hash == 0) return kNone;
-    if (sl.hash == h && sl.str_len == tlen && str_eq<kTopicInline>(t, tlen, sl.pfx, v.strings + sl.str_off)) {
+    if (sl.hash == h && sl.str_len == tlen && str_eq<kTopicInline>(nm, t, tlen, sl.pfx, v.strings + sl.str_off)) {
       if (key_ok(sl.r0_flags, sl.r0_keys_lo, sl.r0_keys_hi, kind) &&
           rest_ok(sl.r0_flags, static_cast<int16_t>(sl.r0_flags >> 16), sl.r0_client, version, true, client))
         return sl.r0_id;
@@ -276,9 +303,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader&
     uint32_t coff, clen;
     rd_str(d, &coff, &clen);
     const uint8_t* client = rec + coff;
-    uint32_t chash = kFnvBasis;
-    for (uint32_t i = 0; i < clen; ++i) chash = fnv1a_step(chash, client[i]);
-    const uint32_t cid = intern_client(v, client, clen, chash);
+    const uint32_t cid = intern_client(v, client, clen);
 
     int32_t ntop = 0;
     bool ok = true;
@@ -452,8 +477,8 @@ __device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits
 
 constexpr uint32_t kKWaves = 16;
 constexpr uint32_t kKBlock = 64 * kKWaves;
-constexpr uint32_t kKMaxStage = 8192;
-constexpr uint32_t kKCopyIters = kKMaxStage / 1024;
+constexpr uint32_t kKMaxStage = 6144;
+constexpr uint32_t kKCopyIters = kKMaxStage / 1024;  // 16-byte loads per lane
 constexpr uint32_t kKLdsBytes = 160 * 1024;
 constexpr uint32_t kKMaxLdsCounters = 16384;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
