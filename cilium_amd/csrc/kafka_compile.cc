@@ -151,10 +151,16 @@ int sanitize(const l7m_kafka_rule& in, KRule* r, std::string* err) {
   return L7M_OK;
 }
 
-uint32_t fnv1a(const std::string& s) {
-  uint32_t h = kFnvBasis;
-  for (unsigned char c : s) h = fnv1a_step(h, c);
-  return h;
+uint32_t name_hash(const std::string& s) {  // program.h name_hash_step
+  const size_t words = std::max<size_t>(kNameHashMinWords, (s.size() + 3) / 4);
+  uint32_t h = 0;
+  for (size_t k = 0; k < words; ++k) {
+    uint32_t w = 0;
+    for (size_t b = 0; b < 4; ++b)
+      if (4 * k + b < s.size()) w |= static_cast<uint32_t>(static_cast<unsigned char>(s[4 * k + b])) << (8 * b);
+    h = name_hash_step(h, w);
+  }
+  return name_hash_final(h, static_cast<uint32_t>(s.size()));
 }
 
 bool key_ok(const KRule& r, uint32_t k) {  // CheckAPIKeyRole for table index k
@@ -255,7 +261,7 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   std::vector<KafkaTopicSlot> slots(n_slots);
   std::memset(slots.data(), 0, slots.size() * sizeof(KafkaTopicSlot));
   for (const auto& kv : by_topic) {
-    uint32_t hk = kafka_key_hash(fnv1a(kv.first));
+    uint32_t hk = name_hash(kv.first);
     uint32_t at = hk & (n_slots - 1);
     while (slots[at].hash != 0) at = (at + 1) & (n_slots - 1);
     KafkaTopicSlot& sl = slots[at];
@@ -276,7 +282,7 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   std::vector<KafkaClientSlot> cslots(n_clients);
   std::memset(cslots.data(), 0, cslots.size() * sizeof(KafkaClientSlot));
   for (const auto& kv : client_ids) {
-    uint32_t hk = kafka_key_hash(fnv1a(kv.first));
+    uint32_t hk = name_hash(kv.first);
     uint32_t at = hk & (n_clients - 1);
     while (cslots[at].hash != 0) at = (at + 1) & (n_clients - 1);
     KafkaClientSlot& sl = cslots[at];

@@ -159,10 +159,10 @@ struct KView {
 // The first 24 bytes of the name t[0..len) as little-endian words, zero
 // past len, from aligned dword reads of the words that hold name bytes
 // (records are dword aligned in both the LDS stage and the arena).
-constexpr uint32_t kNameWords = 6;
+constexpr uint32_t kNameWords = kNameHashMinWords;
 struct Name {
   uint32_t x[kNameWords];
-  uint32_t hash;  // FNV-1a 32 of the whole name
+  uint32_t hash;  // program.h name hash (table key)
 };
 
 __device__ __forceinline__ Name load_name(const uint8_t* t, uint32_t len) {
@@ -172,18 +172,20 @@ __device__ __forceinline__ Name load_name(const uint8_t* t, uint32_t len) {
   uint32_t w[kNameWords + 1];
 #pragma unroll
   for (uint32_t k = 0; k <= kNameWords; ++k) w[k] = 4 * k < sh + len ? a[k] : 0u;
-  uint32_t h = kFnvBasis;
+  uint32_t h = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kNameWords; ++k) {
     const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
     const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
     nm.x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
-#pragma unroll
-    for (uint32_t b = 0; b < 4; ++b)
-      if (static_cast<int32_t>(b) < rem) h = fnv1a_step(h, (nm.x[k] >> (8 * b)) & 0xffu);
+    h = name_hash_step(h, nm.x[k]);
   }
-  for (uint32_t i = 4 * kNameWords; i < len; ++i) h = fnv1a_step(h, t[i]);
-  nm.hash = h;
+  for (uint32_t i = 4 * kNameWords; i < len; i += 4) {  // names longer than 24 bytes
+    uint32_t x = 0;
+    for (uint32_t b = 0; b < 4 && i + b < len; ++b) x |= static_cast<uint32_t>(t[i + b]) << (8 * b);
+    h = name_hash_step(h, x);
+  }
+  nm.hash = name_hash_final(h, len);
   return nm;
 }
 
@@ -237,7 +239,7 @@ __device__ uint32_t first_in(const KView& v, Span s, uint32_t skip, uint32_t lim
 __device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t* c, uint32_t len) {
   if (!len || !v.n_clients) return kNone;
   const Name nm = load_name(c, len);
-  const uint32_t hk = kafka_key_hash(nm.hash);
+  const uint32_t hk = nm.hash;
   for (uint32_t at = hk & (v.n_clients - 1);; at = (at + 1) & (v.n_clients - 1)) {
     const KafkaClientSlot sl = v.clients[at];
     if (sl.hash == 0) return kNone;
@@ -253,7 +255,7 @@ __device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t
                                                 int16_t version, uint32_t client) {
   if (!tlen || !v.n_slots) return kNone;
   const Name nm = load_name(t, tlen);
-  const uint32_t h = kafka_key_hash(nm.hash);
+  const uint32_t h = nm.hash;
   for (uint32_t at = h & (v.n_slots - 1);; at = (at + 1) & (v.n_slots - 1)) {
     const KafkaTopicSlot sl = v.slots[at];
     if (sl.hash == 0) return kNone;
@@ -278,7 +280,8 @@ constexpr uint32_t kTopicQ = 4;
 
 // One record whose first `limit` bytes are readable at rec (LDS stage or HBM).
 // tq: this lane's topic column (kTopicQ entries, stride 64 words) in LDS.
-__device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader& h, const uint8_t* rec,
+// spans: the header's per-kind candidate lists staged in LDS (kSpanLds).
+__device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
                                               uint64_t limit, const uint32_t* crc_tab, uint32_t* tq) {
   if (limit < 4) return L7M_VERDICT_PARSE_ERROR;
   const int32_t msize = static_cast<int32_t>((static_cast<uint32_t>(rec[0]) << 24) |
@@ -296,7 +299,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader&
   if (!typed) {
     // request == nil: matchNonTopicRequests (policy.go:54-70), ClientID ignored.
     const bool topic_kind = kind >= 0 && kind < 64 && ((kTopicApiKeyMask >> kind) & 1ull);
-    first = first_in(v, topic_kind ? h.notopic_by_kind[kidx] : h.all_by_kind[kidx], 0, kNone, kind, false,
+    first = first_in(v, topic_kind ? spans[kidx] : spans[kKafkaKinds + kidx], 0, kNone, kind, false,
                      version, false, kNone);
   } else {
     Rd d{rec, 4u + static_cast<uint32_t>(msize), 12, false};
@@ -446,9 +449,9 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader&
     if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
     if (kind == 10) {
       // ConsumerMetadataReq: GetTopics() is nil and ruleMatches -> true.
-      first = first_in(v, h.all_by_kind[kidx], 0, kNone, kind, false, version, false, kNone);
+      first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, false, kNone);
     } else if (ntop == 0) {
-      first = first_in(v, h.all_by_kind[kidx], 0, kNone, kind, false, version, true, cid);
+      first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, true, cid);
     } else {
       for (uint32_t r = 0; r < nq && maxf != kNone; ++r) {
         const uint32_t toff = tq[64 * r];
@@ -456,7 +459,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const KafkaHeader&
         const uint32_t f = topic_first(v, rec + toff, tlen, kind, version, cid);
         maxf = f > maxf ? f : maxf;
       }
-      const uint32_t j = first_in(v, h.notopic_by_kind[kidx], 0, maxf, kind, false, version, true, cid);
+      const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid);
       first = j < maxf ? j : maxf;
     }
   }
@@ -481,6 +484,7 @@ constexpr uint32_t kKMaxStage = 6144;
 constexpr uint32_t kKCopyIters = kKMaxStage / 1024;  // 16-byte loads per lane
 constexpr uint32_t kKLdsBytes = 160 * 1024;
 constexpr uint32_t kKMaxLdsCounters = 16384;
+constexpr uint32_t kSpanLds = (4 * kKafkaKinds + 3) & ~3u;  // words
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
@@ -514,11 +518,16 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t n_ctr = h.n_rules + 2;
   uint32_t* crc_tab = ksmem;
-  uint32_t* ctr = ksmem + 256;
+  Span* spans = reinterpret_cast<Span*>(ksmem + 256);
+  uint32_t* ctr = ksmem + 256 + kSpanLds;
   uint32_t* tq = ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);
   uint8_t* stg = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ) + wv * (stage + 16u);
   tq += wv * 64 * kTopicQ + lane;
   for (uint32_t i = tid; i < 256; i += kKBlock) crc_tab[i] = prog[h.off_crc + i];
+  static_assert(offsetof(KafkaHeader, all_by_kind) == offsetof(KafkaHeader, notopic_by_kind) + 8 * kKafkaKinds,
+                "span arrays are adjacent");
+  for (uint32_t i = tid; i < 4 * kKafkaKinds; i += kKBlock)
+    ksmem[256 + i] = prog[offsetof(KafkaHeader, notopic_by_kind) / 4 + i];
   if (kHits == kKLdsHits)
     for (uint32_t i = tid; i < n_ctr; i += kKBlock) ctr[i] = 0;
   __syncthreads();
@@ -605,13 +614,13 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka(v, h, rec, onext - o, crc_tab, tq);
+          verdict = eval_kafka(v, spans, rec, onext - o, crc_tab, tq);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka(v, h, arena + o, arena_bytes - o, crc_tab, tq) : L7M_VERDICT_PARSE_ERROR;
+        verdict = inb ? eval_kafka(v, spans, arena + o, arena_bytes - o, crc_tab, tq) : L7M_VERDICT_PARSE_ERROR;
       }
       verdicts[t.cur + lane] = verdict;
     }
@@ -656,7 +665,7 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   if (n == 0) return hipSuccess;
   const uint32_t n_ctr = h.n_rules + 2;
   const int mode = !hits ? kKNoHits : (n_ctr <= kKMaxLdsCounters ? kKLdsHits : kKGlobalHits);
-  const size_t fixed = 4u * (256u + (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u) + kKWaves * 64 * kTopicQ);
+  const size_t fixed = 4u * (256u + kSpanLds + (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u) + kKWaves * 64 * kTopicQ);
   size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
   stage &= ~size_t(15);
   if (stage > kKMaxStage) stage = kKMaxStage;

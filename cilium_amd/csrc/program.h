@@ -137,7 +137,7 @@ struct KafkaRuleDesc {
 constexpr uint32_t kKRuleAnyKey = 1u, kKRuleVersion = 2u, kKRuleTopic = 4u, kKRuleClient = 8u;
 
 // Open-addressed (linear probing) table: Topic -> ascending ids of the rules
-// whose Topic equals it.  hash == 0 marks an empty slot (see kafka_key_hash).
+// whose Topic equals it.  hash == 0 marks an empty slot (see name_hash_final).
 // One 64-byte slot carries the first rule's check fields and the first
 // kTopicInline bytes of the topic (zero padded), so the common case (one
 // rule per topic, short names) resolves with a single slot fetch.
@@ -189,10 +189,29 @@ static_assert(sizeof(KafkaTopicSlot) == 64, "topic slot is 16 words");
 static_assert(sizeof(KafkaClientSlot) == 32, "client slot is 8 words");
 static_assert(sizeof(KafkaHeader) % 16 == 0, "header is whole 16-byte lines");
 
-constexpr uint32_t kFnvBasis = 2166136261u;
-__host__ __device__ inline uint32_t fnv1a_step(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }
-// Table key: FNV-1a 32 with 0 remapped (0 marks an empty slot).
-__host__ __device__ inline uint32_t kafka_key_hash(uint32_t h) { return h ? h : 1u; }
+// Key hash of the Kafka topic / ClientID tables: the name zero-padded to
+// max(len, 24) rounded up to whole words, read as little-endian u32 words,
+// each folded in by a multiply-rotate step (word-wise so that the device
+// hashes the 24-byte prefix it already holds in registers without byte
+// extraction); the length is mixed in last and 0 is remapped (0 marks an
+// empty slot).
+constexpr uint32_t kNameHashMinWords = 6;
+__host__ __device__ inline uint32_t name_hash_step(uint32_t h, uint32_t w) {
+  w *= 0xcc9e2d51u;
+  w = (w << 15) | (w >> 17);
+  h ^= w * 0x1b873593u;
+  h = (h << 13) | (h >> 19);
+  return h * 5u + 0xe6546b64u;
+}
+__host__ __device__ inline uint32_t name_hash_final(uint32_t h, uint32_t len) {
+  h ^= len;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h ? h : 1u;
+}
 
 // isTopicAPIKey (pkg/kafka/policy.go:27-52) as a mask over kinds 0..63.
 constexpr uint64_t kTopicApiKeyMask =
