@@ -55,6 +55,17 @@ __device__ __forceinline__ int8_t rd_i8(Rd& d) { return static_cast<int8_t>(rd_b
 __device__ __forceinline__ int16_t rd_i16(Rd& d) { return static_cast<int16_t>(rd_be(d, 2)); }
 __device__ __forceinline__ int32_t rd_i32(Rd& d) { return static_cast<int32_t>(rd_be(d, 4)); }
 
+// n fixed-size bytes whose value is not needed.
+__device__ __forceinline__ void rd_skip(Rd& d, uint32_t n) {
+  if (d.err) return;
+  if (d.len - d.pos < n) {
+    d.pos = d.len;
+    d.err = true;
+    return;
+  }
+  d.pos += n;
+}
+
 // DecodeString (serialization.go:120-153): *off/*len of the bytes, len 0 = "".
 __device__ __forceinline__ void rd_str(Rd& d, uint32_t* off, uint32_t* len) {
   *off = 0;
@@ -165,13 +176,17 @@ struct Name {
   uint32_t hash;  // program.h name hash (table key)
 };
 
+// kLds: t is in the LDS stage, where reading past the name is harmless, so
+// all seven words are read unconditionally; from HBM only the words that
+// hold name bytes are.
+template <bool kLds>
 __device__ __forceinline__ Name load_name(const uint8_t* t, uint32_t len) {
   Name nm;
   const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(t)) & 3u;
   const uint32_t* a = reinterpret_cast<const uint32_t*>(t - sh);
   uint32_t w[kNameWords + 1];
 #pragma unroll
-  for (uint32_t k = 0; k <= kNameWords; ++k) w[k] = 4 * k < sh + len ? a[k] : 0u;
+  for (uint32_t k = 0; k <= kNameWords; ++k) w[k] = (kLds || 4 * k < sh + len) ? a[k] : 0u;
   uint32_t h = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kNameWords; ++k) {
@@ -236,9 +251,10 @@ __device__ uint32_t first_in(const KView& v, Span s, uint32_t skip, uint32_t lim
 }
 
 // The request ClientID's index among the rules' ClientIDs (kNone if none).
+template <bool kLds>
 __device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t* c, uint32_t len) {
   if (!len || !v.n_clients) return kNone;
-  const Name nm = load_name(c, len);
+  const Name nm = load_name<kLds>(c, len);
   const uint32_t hk = nm.hash;
   for (uint32_t at = hk & (v.n_clients - 1);; at = (at + 1) & (v.n_clients - 1)) {
     const KafkaClientSlot sl = v.clients[at];
@@ -251,10 +267,11 @@ __device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t*
 // First rule whose Topic is t[0..tlen) and whose CheckAPIKeyRole / version /
 // ClientID conditions hold (kNone if none): the per-topic term of the
 // reqTopicsMap coverage walk (policy.go:210-223).
+template <bool kLds>
 __device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t, uint32_t tlen, int32_t kind,
                                                 int16_t version, uint32_t client) {
   if (!tlen || !v.n_slots) return kNone;
-  const Name nm = load_name(t, tlen);
+  const Name nm = load_name<kLds>(t, tlen);
   const uint32_t h = nm.hash;
   for (uint32_t at = h & (v.n_slots - 1);; at = (at + 1) & (v.n_slots - 1)) {
     const KafkaTopicSlot sl = v.slots[at];
@@ -280,7 +297,9 @@ constexpr uint32_t kTopicQ = 4;
 
 // One record whose first `limit` bytes are readable at rec (LDS stage or HBM).
 // tq: this lane's topic column (kTopicQ entries, stride 64 words) in LDS.
-// spans: the header's per-kind candidate lists staged in LDS (kSpanLds).
+// spans: the header's per-kind candidate lists staged in LDS (kSpanLds);
+// kLds: rec is in the LDS stage.
+template <bool kLds>
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
                                               uint64_t limit, const uint32_t* crc_tab, uint32_t* tq) {
   if (limit < 4) return L7M_VERDICT_PARSE_ERROR;
@@ -306,7 +325,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     uint32_t coff, clen;
     rd_str(d, &coff, &clen);
     const uint8_t* client = rec + coff;
-    const uint32_t cid = intern_client(v, client, clen);
+    const uint32_t cid = intern_client<kLds>(v, client, clen);
 
     int32_t ntop = 0;
     bool ok = true;
@@ -323,128 +342,95 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
         tq[64 * nq] = toff;
         ++nq;
       } else {
-        const uint32_t f = topic_first(v, rec + toff, tlen, kind, version, cid);
+        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kind, version, cid);
         maxf = f > maxf ? f : maxf;
       }
     };
-    int32_t n, np;
+    // The per-kind readers (messages.go) share one shape: kind-specific
+    // leading fields, the topic array (name + kind-specific partition
+    // array), kind-specific trailing fields.  Only the leading / trailing
+    // fields and the variable-size partition entries (Produce message sets,
+    // OffsetCommit metadata strings) are decoded per kind; the topic loop is
+    // common, so lanes holding different kinds walk it together.  A run of
+    // fixed-size reads is one rd_skip: under the sticky-error semantics it
+    // fails exactly when one of the reads would.
+    uint32_t a, b;
     switch (kind) {
-      case 0: {  // ReadProduceReq messages.go:1572-1628
-        if (version >= 3) {
-          uint32_t a, b;
-          rd_str(d, &a, &b);
-        }
-        rd_i16(d);
-        rd_i32(d);
-        if (!rd_arraylen(d, &n)) { ok = false; break; }
-        start_topics(n);
-        for (int32_t t = 0; t < n && ok && ms == kMsOk; ++t) {
-          topic();
-          if (!rd_arraylen(d, &np)) { ok = false; break; }
-          for (int32_t p = 0; p < np; ++p) {
-            rd_i32(d);
-            if (d.err) { ok = false; break; }
-            const int32_t mss = rd_i32(d);
-            if (d.err) { ok = false; break; }
-            const int rc = read_message_set(d, mss, version, crc_tab);
-            if (rc == kMsErr) { ok = false; break; }
-            if (rc == kMsUnsupported) { ms = rc; break; }
-          }
-          if (d.err) break;  // remaining iterations are no-ops; Err() fails below
-        }
+      case 0:  // ReadProduceReq messages.go:1572-1628
+        if (version >= 3) rd_str(d, &a, &b);  // transactional id
+        rd_skip(d, 2 + 4);                    // acks, timeout
         break;
-      }
-      case 1: {  // ReadFetchReq messages.go:752-809
-        rd_i32(d);
-        rd_i32(d);
-        rd_i32(d);
-        if (version >= 3) rd_i32(d);
-        if (version >= 4) rd_i8(d);
-        if (!rd_arraylen(d, &n)) { ok = false; break; }
-        start_topics(n);
-        for (int32_t t = 0; t < n && ok; ++t) {
-          topic();
-          if (!rd_arraylen(d, &np)) { ok = false; break; }
-          for (int32_t p = 0; p < np && !d.err; ++p) {
-            rd_i32(d);
-            rd_be(d, 8);
-            if (version >= 5) rd_be(d, 8);
-            rd_i32(d);
-          }
-          if (d.err) break;
-        }
+      case 1:  // ReadFetchReq messages.go:752-809
+        rd_skip(d, 12 + (version >= 3 ? 4 : 0) + (version >= 4 ? 1 : 0));
         break;
-      }
-      case 2: {  // ReadOffsetReq messages.go:1791-1839
-        rd_i32(d);
-        if (version >= 2) rd_i8(d);
-        if (!rd_arraylen(d, &n)) { ok = false; break; }
-        start_topics(n);
-        for (int32_t t = 0; t < n && ok; ++t) {
-          topic();
-          if (!rd_arraylen(d, &np)) { ok = false; break; }
-          for (int32_t p = 0; p < np && !d.err; ++p) {
-            rd_i32(d);
-            rd_be(d, 8);
-            if (version == 0) rd_i32(d);
-          }
-          if (d.err) break;
-        }
+      case 2:  // ReadOffsetReq messages.go:1791-1839
+        rd_skip(d, 4 + (version >= 2 ? 1 : 0));
         break;
-      }
-      case 3: {  // ReadMetadataReq messages.go:493-522
-        if (!rd_arraylen(d, &n)) { ok = false; break; }
-        start_topics(n);
-        for (int32_t t = 0; t < n; ++t) {
-          topic();
-          if (d.err) break;
-        }
-        if (version >= 4) rd_i8(d);
-        break;
-      }
-      case 8: {  // ReadOffsetCommitReq messages.go:1158-1213
-        uint32_t a, b;
+      case 8:  // ReadOffsetCommitReq messages.go:1158-1213
         rd_str(d, &a, &b);
         if (version >= 1) {
-          rd_i32(d);
+          rd_skip(d, 4);
           rd_str(d, &a, &b);
         }
-        if (version >= 2) rd_be(d, 8);
-        if (!rd_arraylen(d, &n)) { ok = false; break; }
-        start_topics(n);
-        for (int32_t t = 0; t < n && ok; ++t) {
-          topic();
-          if (!rd_arraylen(d, &np)) { ok = false; break; }
-          for (int32_t p = 0; p < np && !d.err; ++p) {
-            rd_i32(d);
-            rd_be(d, 8);
-            if (version == 1) rd_be(d, 8);
-            rd_str(d, &a, &b);
+        if (version >= 2) rd_skip(d, 8);
+        break;
+      case 9:  // ReadOffsetFetchReq messages.go:1374-1411
+        rd_str(d, &a, &b);
+        break;
+      case 10:  // ReadConsumerMetadataReq messages.go:1018-1039: no topics
+        rd_str(d, &a, &b);
+        if (version >= 1) rd_skip(d, 1);
+        break;
+      default:  // 3: ReadMetadataReq messages.go:493-522
+        break;
+    }
+    int32_t n = 0;
+    if (kind != 10 && !rd_arraylen(d, &n)) ok = false;
+    start_topics(n);
+    // Fixed partition entry sizes (0: variable or no partition array).
+    const uint32_t esz = kind == 1 ? 16u + (version >= 5 ? 8u : 0u)
+                       : kind == 2 ? 12u + (version == 0 ? 4u : 0u)
+                       : kind == 9 ? 4u : 0u;
+    for (int32_t t = 0; t < n && ok && !d.err; ++t) {
+      topic();
+      if (kind == 3 || d.err) continue;
+      int32_t np;
+      if (!rd_arraylen(d, &np)) {
+        ok = false;
+        break;
+      }
+      if (esz) {
+        const uint64_t need = static_cast<uint64_t>(np) * esz;
+        if (d.len - d.pos < need) {
+          d.pos = d.len;
+          d.err = true;
+        } else {
+          d.pos += static_cast<uint32_t>(need);
+        }
+      } else if (kind == 0) {
+        for (int32_t p = 0; p < np; ++p) {
+          rd_skip(d, 4);  // partition
+          const int32_t mss = rd_i32(d);
+          if (d.err) break;
+          const int rc = read_message_set(d, mss, version, crc_tab);
+          if (rc == kMsErr) {
+            ok = false;
+            break;
           }
-          if (d.err) break;
+          if (rc == kMsUnsupported) {
+            ms = rc;
+            break;
+          }
         }
-        break;
-      }
-      case 9: {  // ReadOffsetFetchReq messages.go:1374-1411
-        uint32_t a, b;
-        rd_str(d, &a, &b);
-        if (!rd_arraylen(d, &n)) { ok = false; break; }
-        start_topics(n);
-        for (int32_t t = 0; t < n && ok; ++t) {
-          topic();
-          if (!rd_arraylen(d, &np)) { ok = false; break; }
-          for (int32_t p = 0; p < np && !d.err; ++p) rd_i32(d);
-          if (d.err) break;
+        if (ms != kMsOk) break;
+      } else {  // 8
+        for (int32_t p = 0; p < np && !d.err; ++p) {
+          rd_skip(d, 4 + 8 + (version == 1 ? 8 : 0));
+          rd_str(d, &a, &b);
         }
-        break;
-      }
-      default: {  // 10: ReadConsumerMetadataReq messages.go:1018-1039
-        uint32_t a, b;
-        rd_str(d, &a, &b);
-        if (version >= 1) rd_i8(d);
-        break;
       }
     }
+    if (kind == 3 && version >= 4) rd_skip(d, 1);
     if (ms == kMsUnsupported) return L7M_VERDICT_UNSUPPORTED;
     if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
     if (kind == 10) {
@@ -456,7 +442,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       for (uint32_t r = 0; r < nq && maxf != kNone; ++r) {
         const uint32_t toff = tq[64 * r];
         const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
-        const uint32_t f = topic_first(v, rec + toff, tlen, kind, version, cid);
+        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kind, version, cid);
         maxf = f > maxf ? f : maxf;
       }
       const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid);
@@ -614,13 +600,13 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka(v, spans, rec, onext - o, crc_tab, tq);
+          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka(v, spans, arena + o, arena_bytes - o, crc_tab, tq) : L7M_VERDICT_PARSE_ERROR;
+        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq) : L7M_VERDICT_PARSE_ERROR;
       }
       verdicts[t.cur + lane] = verdict;
     }

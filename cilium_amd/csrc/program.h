@@ -197,16 +197,11 @@ static_assert(sizeof(KafkaHeader) % 16 == 0, "header is whole 16-byte lines");
 // empty slot).
 constexpr uint32_t kNameHashMinWords = 6;
 __host__ __device__ inline uint32_t name_hash_step(uint32_t h, uint32_t w) {
-  w *= 0xcc9e2d51u;
-  w = (w << 15) | (w >> 17);
-  h ^= w * 0x1b873593u;
-  h = (h << 13) | (h >> 19);
-  return h * 5u + 0xe6546b64u;
+  h = (h ^ w) * 0x9e3779b1u;
+  return h ^ (h >> 15);
 }
 __host__ __device__ inline uint32_t name_hash_final(uint32_t h, uint32_t len) {
-  h ^= len;
-  h ^= h >> 16;
-  h *= 0x85ebca6bu;
+  h = (h ^ len) * 0x85ebca6bu;
   h ^= h >> 13;
   h *= 0xc2b2ae35u;
   h ^= h >> 16;
