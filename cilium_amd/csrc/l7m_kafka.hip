@@ -157,6 +157,19 @@ __device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint
   return rc;
 }
 
+#ifdef L7M_PROF
+// Diagnostic build only: per-lane cycle accumulators (s_memtime).
+#define g_prof_t0 prof[0]
+#define g_prof_dec prof[1]
+#define g_prof_rounds prof[2]
+#define g_prof_client prof[3]
+#define PROF_PARAM , uint64_t (&prof)[5]
+#define PROF_ARG , prof
+#else
+#define PROF_PARAM
+#define PROF_ARG
+#endif
+
 struct KView {
   const uint32_t* prog;
   const KafkaRuleDesc* rules;
@@ -296,12 +309,16 @@ __device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t
 constexpr uint32_t kTopicQ = 4;
 
 // One record whose first `limit` bytes are readable at rec (LDS stage or HBM).
-// tq: this lane's topic column (kTopicQ entries, stride 64 words) in LDS.
+// tq: this lane's topic column in LDS (kTopicQ u16 name offsets, stride 64);
+// used by the LDS-staged path only (stage offsets fit 16 bits).
 // spans: the header's per-kind candidate lists staged in LDS (kSpanLds);
 // kLds: rec is in the LDS stage.
 template <bool kLds>
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
-                                              uint64_t limit, const uint32_t* crc_tab, uint32_t* tq) {
+                                              uint64_t limit, const uint32_t* crc_tab, uint16_t* tq PROF_PARAM) {
+#ifdef L7M_PROF
+  if (kLds) g_prof_t0 = __builtin_amdgcn_s_memtime();
+#endif
   if (limit < 4) return L7M_VERDICT_PARSE_ERROR;
   const int32_t msize = static_cast<int32_t>((static_cast<uint32_t>(rec[0]) << 24) |
                                              (static_cast<uint32_t>(rec[1]) << 16) |
@@ -325,7 +342,13 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     uint32_t coff, clen;
     rd_str(d, &coff, &clen);
     const uint8_t* client = rec + coff;
+#ifdef L7M_PROF
+    const uint64_t tc0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t cid = intern_client<kLds>(v, client, clen);
+#ifdef L7M_PROF
+    if (kLds) g_prof_client += __builtin_amdgcn_s_memtime() - tc0;
+#endif
 
     int32_t ntop = 0;
     bool ok = true;
@@ -338,8 +361,8 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       if (d.err || maxf == kNone) return;
       if (!tlen) {
         maxf = kNone;
-      } else if (nq < kTopicQ) {
-        tq[64 * nq] = toff;
+      } else if (kLds && nq < kTopicQ) {
+        tq[64 * nq] = static_cast<uint16_t>(toff);
         ++nq;
       } else {
         const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kind, version, cid);
@@ -439,6 +462,10 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     } else if (ntop == 0) {
       first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, true, cid);
     } else {
+#ifdef L7M_PROF
+      const uint64_t tr0 = __builtin_amdgcn_s_memtime();
+      if (kLds) g_prof_dec += tr0 - g_prof_t0;
+#endif
       for (uint32_t r = 0; r < nq && maxf != kNone; ++r) {
         const uint32_t toff = tq[64 * r];
         const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
@@ -447,6 +474,9 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       }
       const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid);
       first = j < maxf ? j : maxf;
+#ifdef L7M_PROF
+      if (kLds) g_prof_rounds += __builtin_amdgcn_s_memtime() - tr0;
+#endif
     }
   }
   return first == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(first);
@@ -471,6 +501,7 @@ constexpr uint32_t kKCopyIters = kKMaxStage / 1024;  // 16-byte loads per lane
 constexpr uint32_t kKLdsBytes = 160 * 1024;
 constexpr uint32_t kKMaxLdsCounters = 16384;
 constexpr uint32_t kSpanLds = (4 * kKafkaKinds + 3) & ~3u;  // words
+constexpr uint32_t kMaxCliLdsBytes = 8192;  // client table copied to LDS up to this size
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
@@ -493,22 +524,30 @@ enum KHitMode { kKNoHits = 0, kKLdsHits = 1, kKGlobalHits = 2 };
 // its tile window is decoded from HBM.
 // kAblate (diagnostics only, L7M_FLAG_DIAG_*): 1 = stage records, no
 // decoding; 2 = decode without table lookups.
-template <int kHits, int kAblate>
+template <int kHits, int kAblate, bool kCliLds>
 __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
                                                              const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                              const uint64_t* __restrict__ offs, uint64_t n,
                                                              int32_t* __restrict__ verdicts,
                                                              unsigned long long* __restrict__ hits, uint32_t stage) {
   extern __shared__ __align__(16) uint32_t ksmem[];
+#ifdef L7M_PROF
+  uint64_t prof[5] = {0, 0, 0, 0, 0};
+#endif
   const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t n_ctr = h.n_rules + 2;
+  // LDS: crc | spans | client table (kCliLds) | counters (kKLdsHits) | topic columns | stages
   uint32_t* crc_tab = ksmem;
   Span* spans = reinterpret_cast<Span*>(ksmem + 256);
-  uint32_t* ctr = ksmem + 256 + kSpanLds;
-  uint32_t* tq = ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);
+  uint32_t* cli = ksmem + 256 + kSpanLds;
+  const uint32_t cli_words = kCliLds ? h.n_clients * (sizeof(KafkaClientSlot) / 4) : 0u;
+  uint32_t* ctr = cli + cli_words;
+  uint16_t* tq = reinterpret_cast<uint16_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
   uint8_t* stg = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ) + wv * (stage + 16u);
   tq += wv * 64 * kTopicQ + lane;
+  if (kCliLds)
+    for (uint32_t i = tid; i < cli_words; i += kKBlock) cli[i] = prog[h.off_clients + i];
   for (uint32_t i = tid; i < 256; i += kKBlock) crc_tab[i] = prog[h.off_crc + i];
   static_assert(offsetof(KafkaHeader, all_by_kind) == offsetof(KafkaHeader, notopic_by_kind) + 8 * kKafkaKinds,
                 "span arrays are adjacent");
@@ -521,7 +560,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   v.prog = prog;
   v.rules = reinterpret_cast<const KafkaRuleDesc*>(prog + h.off_rules);
   v.slots = reinterpret_cast<const KafkaTopicSlot*>(prog + h.off_slots);
-  v.clients = reinterpret_cast<const KafkaClientSlot*>(prog + h.off_clients);
+  v.clients = reinterpret_cast<const KafkaClientSlot*>(kCliLds ? cli : prog + h.off_clients);
   v.n_clients = kAblate == 2 ? 0 : h.n_clients;
   v.pool = prog + h.off_pool;
   v.strings = reinterpret_cast<const uint8_t*>(prog + h.off_strings);
@@ -590,6 +629,9 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
 
     const uint64_t o = t.o, onext = t.onext;
     int32_t verdict = 0;
+#ifdef L7M_PROF
+    const uint64_t te0 = __builtin_amdgcn_s_memtime();
+#endif
     if (lane < t.take) {
       bool done = false;
       if (lane < t.k && onext - o >= 4) {
@@ -600,16 +642,19 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq);
+          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq PROF_ARG);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq) : L7M_VERDICT_PARSE_ERROR;
+        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
       }
       verdicts[t.cur + lane] = verdict;
     }
+#ifdef L7M_PROF
+    prof[4] += __builtin_amdgcn_s_memtime() - te0;
+#endif
     if (kHits != kKNoHits) {
       uint32_t slot = kNone;
       if (lane < t.take) slot = verdict >= 0 ? static_cast<uint32_t>(verdict) + 2 : (verdict == -1 ? 0u : 1u);
@@ -622,6 +667,18 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     wave_sync();  // the stage is overwritten by the next tile
     t = t2;
   }
+#ifdef L7M_PROF
+  if (blockIdx.x == 0 && wv == 0) {
+    for (int k = 0; k < 5; ++k)
+      for (uint32_t m = 1; m < 64; m <<= 1) {
+        const uint64_t o2 = shfl64(prof[k], lane ^ m);
+        prof[k] = o2 > prof[k] ? o2 : prof[k];
+      }
+    if (lane == 0)
+      printf("L7M_PROF decode %llu client %llu rounds %llu eval %llu\n", (unsigned long long)prof[1],
+             (unsigned long long)prof[3], (unsigned long long)prof[2], (unsigned long long)prof[4]);
+  }
+#endif
   if (kHits == kKLdsHits) {
     __syncthreads();
     for (uint32_t i = tid; i < n_ctr; i += kKBlock)
@@ -629,17 +686,17 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   }
 }
 
-template <int kHits, int kAblate = 0>
+template <int kHits, int kAblate = 0, bool kCliLds = false>
 static void launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                      uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                      unsigned long long* hits, uint32_t stage) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate, kCliLds>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kKLdsBytes);
     attr_set = true;
   }
-  hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate>), grid, dim3(kKBlock), lds, stream, dprog, arena, arena_bytes, offs,
+  hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate, kCliLds>), grid, dim3(kKBlock), lds, stream, dprog, arena, arena_bytes, offs,
                      n, verdicts, hits, stage);
 }
 
@@ -651,7 +708,11 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   if (n == 0) return hipSuccess;
   const uint32_t n_ctr = h.n_rules + 2;
   const int mode = !hits ? kKNoHits : (n_ctr <= kKMaxLdsCounters ? kKLdsHits : kKGlobalHits);
-  const size_t fixed = 4u * (256u + kSpanLds + (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u) + kKWaves * 64 * kTopicQ);
+  const size_t cli_words = static_cast<size_t>(h.n_clients) * (sizeof(KafkaClientSlot) / 4);
+  const bool cli_lds = cli_words && cli_words * 4 <= kMaxCliLdsBytes;
+  const size_t fixed = 4u * (256u + kSpanLds + (cli_lds ? cli_words : 0u) +
+                             (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
+                       2u * kKWaves * 64 * kTopicQ;
   size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
   stage &= ~size_t(15);
   if (stage > kKMaxStage) stage = kKMaxStage;
@@ -668,9 +729,18 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
       launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
     return hipGetLastError();
   }
-  if (mode == kKNoHits) launch_k<kKNoHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
-  else if (mode == kKLdsHits) launch_k<kKLdsHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
-  else launch_k<kKGlobalHits>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
+#define L7M_KAFKA_LAUNCH(M, C) \
+  launch_k<M, 0, C>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st)
+  if (cli_lds) {
+    if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, true);
+    else if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, true);
+    else L7M_KAFKA_LAUNCH(kKGlobalHits, true);
+  } else {
+    if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, false);
+    else if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, false);
+    else L7M_KAFKA_LAUNCH(kKGlobalHits, false);
+  }
+#undef L7M_KAFKA_LAUNCH
   return hipGetLastError();
 }
 
