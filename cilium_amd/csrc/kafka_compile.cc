@@ -257,25 +257,42 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   auto put_prefix = [](uint32_t* pfx, size_t cap, const std::string& s) {
     std::memcpy(pfx, s.data(), std::min(cap, s.size()));
   };
+  // Distinct apiKey sets; id 0 = any kind.
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> kset_ids;
+  std::vector<uint64_t> kset_masks(1, ~0ull);
+  auto kset_of = [&](const KafkaRuleDesc& d) -> uint32_t {
+    if (d.flags & kKRuleAnyKey) return 0;
+    auto it = kset_ids.emplace(std::make_pair(d.keys_lo, d.keys_hi), static_cast<uint32_t>(kset_masks.size()));
+    if (it.second) kset_masks.push_back((static_cast<uint64_t>(d.keys_hi) << 32) | d.keys_lo);
+    return it.first->second;
+  };
   const uint32_t n_slots = table_size(by_topic.size());
   std::vector<KafkaTopicSlot> slots(n_slots);
+  std::vector<KafkaTopicExt> ext(n_slots);
   std::memset(slots.data(), 0, slots.size() * sizeof(KafkaTopicSlot));
+  std::memset(ext.data(), 0, ext.size() * sizeof(KafkaTopicExt));
   for (const auto& kv : by_topic) {
-    uint32_t hk = name_hash(kv.first);
+    const uint32_t hk = name_hash(kv.first);
     uint32_t at = hk & (n_slots - 1);
     while (slots[at].hash != 0) at = (at + 1) & (n_slots - 1);
     KafkaTopicSlot& sl = slots[at];
-    sl.hash = hk;
-    sl.str_off = put_str(kv.first);
-    sl.str_len = static_cast<uint32_t>(kv.first.size());
-    sl.rules = push_list(kv.second);
     const KafkaRuleDesc& d = desc[kv.second[0]];
-    sl.r0_id = kv.second[0];
-    sl.r0_flags = d.flags | (static_cast<uint32_t>(static_cast<uint16_t>(d.version)) << 16);
-    sl.r0_keys_lo = d.keys_lo;
-    sl.r0_keys_hi = d.keys_hi;
+    sl.hash = hk;
+    sl.meta = static_cast<uint32_t>(kv.first.size()) | (kset_of(d) << 8) |
+              ((d.flags & kKRuleVersion) ? kSlotVersionCond : 0u) | ((d.flags & kKRuleClient) ? kSlotClientCond : 0u) |
+              (static_cast<uint32_t>(static_cast<uint16_t>(d.version)) << 16);
+    sl.r0 = kv.second[0] | (kv.second.size() > 1 ? kSlotMore : 0u);
     sl.r0_client = d.client_idx;
     put_prefix(sl.pfx, kTopicInline, kv.first);
+    ext[at].str_off = put_str(kv.first);
+    ext[at].rules = push_list(kv.second);
+  }
+  if (kset_masks.size() > kMaxKsets) return fail(L7M_ETOOBIG, "too many distinct apiKey sets");
+  uint64_t kind_ok[kKafkaKinds];
+  for (uint32_t k = 0; k < kKafkaKinds; ++k) {
+    kind_ok[k] = 1;  // kset 0: any kind
+    for (uint32_t s = 1; s < kset_masks.size(); ++s)
+      if (k < 64 && ((kset_masks[s] >> k) & 1)) kind_ok[k] |= 1ull << s;
   }
 
   const uint32_t n_clients = table_size(client_ids.size());
@@ -310,6 +327,8 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   h.off_rules = take(static_cast<uint64_t>(n) * sizeof(KafkaRuleDesc) / 4);
   h.off_slots = take(static_cast<uint64_t>(n_slots) * sizeof(KafkaTopicSlot) / 4);
   h.n_slots = n_slots;
+  h.off_ext = take(static_cast<uint64_t>(n_slots) * sizeof(KafkaTopicExt) / 4);
+  h.off_kind_ok = take(2 * kKafkaKinds);
   h.off_clients = take(static_cast<uint64_t>(n_clients) * sizeof(KafkaClientSlot) / 4);
   h.n_clients = n_clients;
   h.off_pool = take(pool.size());
@@ -322,6 +341,8 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   std::memcpy(prog.data(), &h, sizeof h);
   if (n) std::memcpy(prog.data() + h.off_rules, desc.data(), n * sizeof(KafkaRuleDesc));
   if (n_slots) std::memcpy(prog.data() + h.off_slots, slots.data(), n_slots * sizeof(KafkaTopicSlot));
+  if (n_slots) std::memcpy(prog.data() + h.off_ext, ext.data(), n_slots * sizeof(KafkaTopicExt));
+  std::memcpy(prog.data() + h.off_kind_ok, kind_ok, sizeof kind_ok);
   if (n_clients)
     std::memcpy(prog.data() + h.off_clients, cslots.data(), n_clients * sizeof(KafkaClientSlot));
   if (!pool.empty()) std::memcpy(prog.data() + h.off_pool, pool.data(), pool.size() * 4);

@@ -174,6 +174,8 @@ struct KView {
   const uint32_t* prog;
   const KafkaRuleDesc* rules;
   const KafkaTopicSlot* slots;
+  const KafkaTopicExt* ext;
+  const uint64_t* kind_ok;  // LDS copy of the program's kind_ok table
   const KafkaClientSlot* clients;
   const uint32_t* pool;
   const uint8_t* strings;
@@ -277,25 +279,50 @@ __device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t*
   }
 }
 
+// The topic's first rule whose CheckAPIKeyRole / version / ClientID
+// conditions hold, once slot `at` is known to hold the topic: its first rule
+// from the slot's own fields, later ones from the pool (kNone if none).
+// kok: the request kind's kind_ok bits.
+__device__ __forceinline__ uint32_t slot_first(const KView& v, const KafkaTopicSlot& sl, uint32_t at, uint64_t kok,
+                                               int32_t kind, int16_t version, uint32_t client) {
+  const uint32_t m = sl.meta;
+  if (((kok >> ((m >> 8) & 63u)) & 1ull) &&
+      (!(m & kSlotVersionCond) || static_cast<int16_t>(m >> 16) == version) &&
+      (!(m & kSlotClientCond) || sl.r0_client == client))
+    return sl.r0 & ~kSlotMore;
+  if (!(sl.r0 & kSlotMore)) return kNone;
+  return first_in(v, v.ext[at].rules, 1, kNone, kind, true, version, true, client);
+}
+
+// Does slot `at` hold the name nm == t[0..tlen)?
+__device__ __forceinline__ bool slot_is(const KView& v, const KafkaTopicSlot& sl, uint32_t at, uint32_t hash,
+                                        const Name& nm, const uint8_t* t, uint32_t tlen) {
+  if (sl.hash != hash || (sl.meta & 0xffu) != tlen) return false;
+  const uint8_t* rest = tlen > kTopicInline ? v.strings + v.ext[at].str_off : nullptr;
+  return str_eq<kTopicInline>(nm, t, tlen, sl.pfx, rest);
+}
+
+// Probe from slot `at` (already fetched as sl) for the name nm.
+__device__ __forceinline__ uint32_t probe_topic(const KView& v, KafkaTopicSlot sl, uint32_t hash, const Name& nm,
+                                                const uint8_t* t, uint32_t tlen, uint64_t kok, int32_t kind,
+                                                int16_t version, uint32_t client) {
+  for (uint32_t at = hash & (v.n_slots - 1);;) {
+    if (sl.hash == 0) return kNone;
+    if (slot_is(v, sl, at, hash, nm, t, tlen)) return slot_first(v, sl, at, kok, kind, version, client);
+    at = (at + 1) & (v.n_slots - 1);
+    sl = v.slots[at];
+  }
+}
+
 // First rule whose Topic is t[0..tlen) and whose CheckAPIKeyRole / version /
 // ClientID conditions hold (kNone if none): the per-topic term of the
 // reqTopicsMap coverage walk (policy.go:210-223).
 template <bool kLds>
-__device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t, uint32_t tlen, int32_t kind,
-                                                int16_t version, uint32_t client) {
-  if (!tlen || !v.n_slots) return kNone;
+__device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t, uint32_t tlen, uint64_t kok,
+                                                int32_t kind, int16_t version, uint32_t client) {
+  if (!tlen || tlen > kMaxTopicLen || !v.n_slots) return kNone;
   const Name nm = load_name<kLds>(t, tlen);
-  const uint32_t h = nm.hash;
-  for (uint32_t at = h & (v.n_slots - 1);; at = (at + 1) & (v.n_slots - 1)) {
-    const KafkaTopicSlot sl = v.slots[at];
-    if (sl.hash == 0) return kNone;
-    if (sl.hash == h && sl.str_len == tlen && str_eq<kTopicInline>(nm, t, tlen, sl.pfx, v.strings + sl.str_off)) {
-      if (key_ok(sl.r0_flags, sl.r0_keys_lo, sl.r0_keys_hi, kind) &&
-          rest_ok(sl.r0_flags, static_cast<int16_t>(sl.r0_flags >> 16), sl.r0_client, version, true, client))
-        return sl.r0_id;
-      return sl.rules.len > 1 ? first_in(v, sl.rules, 1, kNone, kind, true, version, true, client) : kNone;
-    }
-  }
+  return probe_topic(v, v.slots[nm.hash & (v.n_slots - 1)], nm.hash, nm, t, tlen, kok, kind, version, client);
 }
 
 // Topics are resolved after the decode, all lanes of the wave together
@@ -346,6 +373,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     const uint64_t tc0 = __builtin_amdgcn_s_memtime();
 #endif
     const uint32_t cid = intern_client<kLds>(v, client, clen);
+    const uint64_t kok = v.kind_ok[kidx];
 #ifdef L7M_PROF
     if (kLds) g_prof_client += __builtin_amdgcn_s_memtime() - tc0;
 #endif
@@ -365,7 +393,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
         tq[64 * nq] = static_cast<uint16_t>(toff);
         ++nq;
       } else {
-        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kind, version, cid);
+        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid);
         maxf = f > maxf ? f : maxf;
       }
     };
@@ -469,7 +497,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       for (uint32_t r = 0; r < nq && maxf != kNone; ++r) {
         const uint32_t toff = tq[64 * r];
         const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
-        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kind, version, cid);
+        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid);
         maxf = f > maxf ? f : maxf;
       }
       const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid);
@@ -501,6 +529,7 @@ constexpr uint32_t kKCopyIters = kKMaxStage / 1024;  // 16-byte loads per lane
 constexpr uint32_t kKLdsBytes = 160 * 1024;
 constexpr uint32_t kKMaxLdsCounters = 16384;
 constexpr uint32_t kSpanLds = (4 * kKafkaKinds + 3) & ~3u;  // words
+constexpr uint32_t kKindOkLds = (2 * kKafkaKinds + 3) & ~3u;  // words
 constexpr uint32_t kMaxCliLdsBytes = 8192;  // client table copied to LDS up to this size
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -537,10 +566,11 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t n_ctr = h.n_rules + 2;
-  // LDS: crc | spans | client table (kCliLds) | counters (kKLdsHits) | topic columns | stages
+  // LDS: crc | spans | kind_ok | client table (kCliLds) | counters (kKLdsHits) | topic columns | stages
   uint32_t* crc_tab = ksmem;
   Span* spans = reinterpret_cast<Span*>(ksmem + 256);
-  uint32_t* cli = ksmem + 256 + kSpanLds;
+  uint64_t* kind_ok = reinterpret_cast<uint64_t*>(ksmem + 256 + kSpanLds);
+  uint32_t* cli = ksmem + 256 + kSpanLds + kKindOkLds;
   const uint32_t cli_words = kCliLds ? h.n_clients * (sizeof(KafkaClientSlot) / 4) : 0u;
   uint32_t* ctr = cli + cli_words;
   uint16_t* tq = reinterpret_cast<uint16_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
@@ -548,6 +578,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   tq += wv * 64 * kTopicQ + lane;
   if (kCliLds)
     for (uint32_t i = tid; i < cli_words; i += kKBlock) cli[i] = prog[h.off_clients + i];
+  for (uint32_t i = tid; i < 2 * kKafkaKinds; i += kKBlock) ksmem[256 + kSpanLds + i] = prog[h.off_kind_ok + i];
   for (uint32_t i = tid; i < 256; i += kKBlock) crc_tab[i] = prog[h.off_crc + i];
   static_assert(offsetof(KafkaHeader, all_by_kind) == offsetof(KafkaHeader, notopic_by_kind) + 8 * kKafkaKinds,
                 "span arrays are adjacent");
@@ -560,6 +591,8 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   v.prog = prog;
   v.rules = reinterpret_cast<const KafkaRuleDesc*>(prog + h.off_rules);
   v.slots = reinterpret_cast<const KafkaTopicSlot*>(prog + h.off_slots);
+  v.ext = reinterpret_cast<const KafkaTopicExt*>(prog + h.off_ext);
+  v.kind_ok = kind_ok;
   v.clients = reinterpret_cast<const KafkaClientSlot*>(kCliLds ? cli : prog + h.off_clients);
   v.n_clients = kAblate == 2 ? 0 : h.n_clients;
   v.pool = prog + h.off_pool;
@@ -710,7 +743,7 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const int mode = !hits ? kKNoHits : (n_ctr <= kKMaxLdsCounters ? kKLdsHits : kKGlobalHits);
   const size_t cli_words = static_cast<size_t>(h.n_clients) * (sizeof(KafkaClientSlot) / 4);
   const bool cli_lds = cli_words && cli_words * 4 <= kMaxCliLdsBytes;
-  const size_t fixed = 4u * (256u + kSpanLds + (cli_lds ? cli_words : 0u) +
+  const size_t fixed = 4u * (256u + kSpanLds + kKindOkLds + (cli_lds ? cli_words : 0u) +
                              (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
                        2u * kKWaves * 64 * kTopicQ;
   size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;

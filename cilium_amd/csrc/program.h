@@ -138,21 +138,29 @@ constexpr uint32_t kKRuleAnyKey = 1u, kKRuleVersion = 2u, kKRuleTopic = 4u, kKRu
 
 // Open-addressed (linear probing) table: Topic -> ascending ids of the rules
 // whose Topic equals it.  hash == 0 marks an empty slot (see name_hash_final).
-// One 64-byte slot carries the first rule's check fields and the first
-// kTopicInline bytes of the topic (zero padded), so the common case (one
-// rule per topic, short names) resolves with a single slot fetch.
-constexpr uint32_t kTopicInline = 24;
+// One 32-byte slot carries the check fields of the topic's first rule and
+// the first kTopicInline bytes of the topic (zero padded), so the common
+// case (short names, first rule decides) resolves with one slot fetch; the
+// rest lives in the parallel KafkaTopicExt array.
+constexpr uint32_t kTopicInline = 16;
 struct KafkaTopicSlot {
   uint32_t hash;
-  uint32_t str_len;
-  uint32_t str_off;      // whole topic in the string area
-  Span rules;            // ascending rule ids in the u32 pool
-  uint32_t r0_id;        // == pool[rules.off]
-  uint32_t r0_flags;     // flags | (uint16)version << 16
-  uint32_t r0_keys_lo, r0_keys_hi;
-  uint32_t r0_client;    // client_idx
+  uint32_t meta;       // len (8) | kset (6) << 8 | version-cond << 14 | client-cond << 15 | (u16)version << 16
+  uint32_t r0;         // first rule id | (more than one rule) << 31
+  uint32_t r0_client;  // its client_idx
   uint32_t pfx[kTopicInline / 4];
 };
+struct KafkaTopicExt {
+  uint32_t str_off;  // whole topic in the string area
+  Span rules;        // ascending rule ids in the u32 pool
+  uint32_t pad;
+};
+constexpr uint32_t kSlotVersionCond = 1u << 14, kSlotClientCond = 1u << 15, kSlotMore = 1u << 31;
+// Rule topics are at most 255 bytes (Sanitize, rule_validation.go:222-226).
+constexpr uint32_t kMaxTopicLen = 255;
+// Distinct apiKey sets ("ksets"): id 0 = any kind; the kind_ok table holds,
+// per request kind (0..63, 64 = other), a bit per kset id that accepts it.
+constexpr uint32_t kMaxKsets = 64;
 
 // Interned rule ClientIDs: one lookup per request turns its ClientID into
 // the index a rule's client_idx is compared with.
@@ -179,13 +187,16 @@ struct KafkaHeader {
   uint32_t total_words;
   uint32_t off_clients;  // KafkaClientSlot[n_clients]
   uint32_t n_clients;    // power of two (0 when no rule has a ClientID)
-  uint32_t pad[5];
+  uint32_t off_ext;      // KafkaTopicExt[n_slots]
+  uint32_t off_kind_ok;  // u64[kKafkaKinds]
+  uint32_t pad[3];
   // Ascending ids of the rules whose CheckAPIKeyRole(kind) holds:
   Span notopic_by_kind[kKafkaKinds];  // ... and Topic == ""
   Span all_by_kind[kKafkaKinds];      // ... any Topic
 };
 static_assert(sizeof(KafkaRuleDesc) == 32, "rule desc is 8 words");
-static_assert(sizeof(KafkaTopicSlot) == 64, "topic slot is 16 words");
+static_assert(sizeof(KafkaTopicSlot) == 32, "topic slot is 8 words");
+static_assert(sizeof(KafkaTopicExt) == 16, "topic ext is 4 words");
 static_assert(sizeof(KafkaClientSlot) == 32, "client slot is 8 words");
 static_assert(sizeof(KafkaHeader) % 16 == 0, "header is whole 16-byte lines");
 
