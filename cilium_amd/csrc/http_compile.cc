@@ -451,6 +451,19 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   const uint32_t lds_dfas = img_take(static_cast<uint64_t>(ndt) * sizeof(DfaDesc) / 4);
   const uint32_t lds_fields = img_take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
   const uint32_t lds_name_field = img_take(name_field.size());
+  // header-name table (always resident when it fits)
+  uint32_t lds_name_tab = kNone, name_slots = 0;
+  std::vector<uint32_t> name_off;
+  if (has_name) {
+    name_slots = 2;
+    while (name_slots < 2 * (nf - 3)) name_slots <<= 1;
+    uint64_t words = 4ull * name_slots;
+    for (uint32_t f = 3; f < nf; ++f) words += ((field_names[f].size() + 3) / 4 + 3) & ~size_t(3);
+    if (4 * words <= kMaxNameTabBytes) {
+      lds_name_tab = img_take(4ull * name_slots);
+      for (uint32_t f = 3; f < nf; ++f) name_off.push_back(img_take((field_names[f].size() + 3) / 4));
+    }
+  }
   for (uint32_t k = 0; k < ndfa; ++k) dd[k].lds_ctmask = img_take((ct[k].size() + 31) / 32);
   auto hotness = [&](uint32_t k) -> int {
     const uint32_t f = all[k].field;
@@ -522,6 +535,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   h.lds_dfas = lds_dfas;
   h.lds_fields = lds_fields;
   h.lds_name_field = lds_name_field;
+  h.lds_name_tab = lds_name_tab;
+  h.name_tab_mask = lds_name_tab != kNone ? name_slots - 1 : 0;
   if (w >= (1ull << 32)) return fail(L7M_ETOOBIG, "program exceeds 16 GiB");
   h.total_words = static_cast<uint32_t>(w);
 
@@ -565,6 +580,20 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   std::memcpy(I + lds_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
   std::memcpy(P + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));
   std::memcpy(I + lds_fields, fd.data(), fd.size() * sizeof(FieldDesc));
+  if (lds_name_tab != kNone) {
+    for (uint32_t f = 3; f < nf; ++f) {
+      const std::string& nm = field_names[f];
+      const uint32_t hk = name_hash(nm);
+      uint32_t at = hk & (name_slots - 1);
+      while (I[lds_name_tab + 4 * at] != 0) at = (at + 1) & (name_slots - 1);
+      uint32_t* sl = I + lds_name_tab + 4 * at;
+      sl[0] = hk;
+      sl[1] = static_cast<uint32_t>(nm.size());
+      sl[2] = f;
+      sl[3] = name_off[f - 3];
+      std::memcpy(I + name_off[f - 3], nm.data(), nm.size());
+    }
+  }
   if (!name_field.empty()) {
     std::memcpy(P + h.off_name_field, name_field.data(), name_field.size() * 4);
     std::memcpy(I + lds_name_field, name_field.data(), name_field.size() * 4);

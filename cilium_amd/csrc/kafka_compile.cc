@@ -151,17 +151,6 @@ int sanitize(const l7m_kafka_rule& in, KRule* r, std::string* err) {
   return L7M_OK;
 }
 
-uint32_t name_hash(const std::string& s) {  // program.h name_hash_step
-  const size_t words = std::max<size_t>(kNameHashMinWords, (s.size() + 3) / 4);
-  uint32_t h = 0;
-  for (size_t k = 0; k < words; ++k) {
-    uint32_t w = 0;
-    for (size_t b = 0; b < 4; ++b)
-      if (4 * k + b < s.size()) w |= static_cast<uint32_t>(static_cast<unsigned char>(s[4 * k + b])) << (8 * b);
-    h = name_hash_step(h, w);
-  }
-  return name_hash_final(h, static_cast<uint32_t>(s.size()));
-}
 
 bool key_ok(const KRule& r, uint32_t k) {  // CheckAPIKeyRole for table index k
   if (r.keys.empty()) return true;

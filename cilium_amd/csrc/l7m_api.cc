@@ -67,7 +67,7 @@ int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
     size_t bytes = rs->program.size() * 4;
     if (hipMalloc(&p, bytes) != hipSuccess) return L7M_ENOMEM;
     if (hipMemcpy(p, rs->program.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      hipFree(p);
+      (void)hipFree(p);
       return L7M_EDEVICE;
     }
     rs->dprog[dev] = p;
@@ -147,10 +147,10 @@ void l7m_release(l7m_ruleset* rs) {
   for (int d = 0; d < 64; ++d)
     if (rs->dprog[d]) {
       int cur = 0;
-      hipGetDevice(&cur);
-      hipSetDevice(d);
-      hipFree(rs->dprog[d]);
-      hipSetDevice(cur);
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(d);
+      (void)hipFree(rs->dprog[d]);
+      (void)hipSetDevice(cur);
     }
   delete rs;
 }
@@ -278,10 +278,10 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
   void *da = nullptr, *doff = nullptr, *dv = nullptr, *dh = nullptr;
   int rc = L7M_OK;
   auto cleanup = [&]() {
-    if (da) hipFree(da);
-    if (doff) hipFree(doff);
-    if (dv) hipFree(dv);
-    if (dh) hipFree(dh);
+    if (da) (void)hipFree(da);
+    if (doff) (void)hipFree(doff);
+    if (dv) (void)hipFree(dv);
+    if (dh) (void)hipFree(dh);
     hipStreamDestroy(st);
   };
   // Pad the arena copy so that the kernels' aligned word loads never run past it.

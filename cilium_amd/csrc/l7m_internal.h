@@ -1,5 +1,6 @@
 // l7m_internal.h — host-side pieces shared by the compilers and the C ABI.
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <mutex>
@@ -7,8 +8,23 @@
 #include <vector>
 
 #include "../../include/l7match.h"
+#include "program.h"
 
 namespace l7m {
+
+// program.h name hash of a host string (Kafka topic / ClientID tables, HTTP
+// header-name table).
+inline uint32_t name_hash(const std::string& s) {
+  const size_t words = std::max<size_t>(kNameHashMinWords, (s.size() + 3) / 4);
+  uint32_t h = 0;
+  for (size_t k = 0; k < words; ++k) {
+    uint32_t w = 0;
+    for (size_t b = 0; b < 4; ++b)
+      if (4 * k + b < s.size()) w |= static_cast<uint32_t>(static_cast<unsigned char>(s[4 * k + b])) << (8 * b);
+    h = name_hash_step(h, w);
+  }
+  return name_hash_final(h, static_cast<uint32_t>(s.size()));
+}
 
 constexpr uint32_t kDefaultLdsBudget = 48u * 1024u;  // bytes of DFA tables in the LDS image
 constexpr uint32_t kLdsCtBudget = 24u * 1024u;       // ... including candidate tables

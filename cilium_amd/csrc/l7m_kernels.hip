@@ -41,11 +41,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Where a record's bytes are read from.
 struct LdsSrc {
+  static constexpr bool kLds = true;
   const uint32_t* w;  // word 0 of the record in the wave's LDS stage
   __device__ __forceinline__ uint32_t word(uint32_t i) const { return w[i]; }
   __device__ __forceinline__ uint32_t byte(uint32_t i) const { return reinterpret_cast<const uint8_t*>(w)[i]; }
 };
 struct GlbSrc {
+  static constexpr bool kLds = false;
   const uint32_t* w;  // word 0 of the record in HBM
   __device__ __forceinline__ uint32_t word(uint32_t i) const { return __builtin_nontemporal_load(w + i); }
   __device__ __forceinline__ uint32_t byte(uint32_t i) const { return reinterpret_cast<const uint8_t*>(w)[i]; }
@@ -183,6 +185,48 @@ __device__ __forceinline__ uint32_t walk_dfa(const Ctx& c, uint32_t d, const Src
   return walk<false>(c.img, c.prog, dd, src, pos, len);
 }
 
+// Field id of the header name at byte `pos` (length len) of the record, via
+// the LDS header-name table (program.h): the name's words are read aligned
+// and hashed word-wise, one slot probe, one word-wise compare.  kNone if no
+// rule references the name.
+template <class Src>
+__device__ __forceinline__ uint32_t name_field_of(const Ctx& c, const HttpHeader& h, const Src& src, uint32_t pos,
+                                                  uint32_t len) {
+  constexpr uint32_t kW = kNameHashMinWords;
+  const uint32_t sh = pos & 3u, w0 = pos >> 2;
+  uint32_t w[kW + 1], x[kW];
+#pragma unroll
+  for (uint32_t k = 0; k <= kW; ++k) w[k] = (Src::kLds || 4 * k < sh + len) ? src.word(w0 + k) : 0u;
+  uint32_t hh = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kW; ++k) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
+    x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+    hh = name_hash_step(hh, x[k]);
+  }
+  for (uint32_t i = 4 * kW; i < len; i += 4) {  // names longer than 24 bytes
+    uint32_t y = 0;
+    for (uint32_t b = 0; b < 4 && i + b < len; ++b) y |= src.byte(pos + i + b) << (8 * b);
+    hh = name_hash_step(hh, y);
+  }
+  hh = name_hash_final(hh, len);
+  const uint32_t* tab = c.img + h.lds_name_tab;
+  for (uint32_t at = hh & h.name_tab_mask;; at = (at + 1) & h.name_tab_mask) {
+    const u32x4 sl = reinterpret_cast<const u32x4*>(tab)[at];
+    if (sl.x == 0) return kNone;
+    if (sl.x != hh || sl.y != len) continue;
+    const uint32_t* nw = c.img + sl.w;
+    bool eq = true;
+#pragma unroll
+    for (uint32_t k = 0; k < kW; ++k)
+      if (4 * k < len) eq &= x[k] == nw[k];
+    for (uint32_t i = 4 * kW; eq && i < len; ++i)
+      eq = src.byte(pos + i) == reinterpret_cast<const uint8_t*>(nw)[i];
+    if (eq) return sl.z;
+  }
+}
+
 // Does end code `code` of DFA d contain pattern p?
 __device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code, uint32_t p) {
   if (code == 0) return false;
@@ -195,11 +239,36 @@ __device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code
   return set_has(c.pool, c.sets[dd.set_base + code], p);
 }
 
+#ifdef L7M_PROF
+// Diagnostic build only: per-lane cycle accumulators per evaluation phase
+// (s_memtime), LDS-staged records only.  prof[0] = last timestamp.
+#define PROF_PARAM , uint64_t (&prof)[8]
+#define PROF_ARG , prof
+#define HPROF(i)                                      \
+  do {                                                \
+    if (Src::kLds) {                                  \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      prof[i] += t_ - prof[0];                        \
+      prof[0] = t_;                                   \
+    }                                                 \
+  } while (0)
+#else
+#define PROF_PARAM
+#define PROF_ARG
+#define HPROF(i) \
+  do {           \
+  } while (0)
+#endif
+
 // Full evaluation of one record whose first `limit` bytes are readable.
 // kAblate (diagnostic builds selected by L7M_FLAG_DIAG_*; verdicts invalid):
 // 1 = stop after the DFA walks, 2 = stop after record validation.
 template <bool kReg, int kAblate, class Src>
-__device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit, uint32_t* col) {
+__device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit,
+                                               uint32_t* col PROF_PARAM) {
+#ifdef L7M_PROF
+  if (Src::kLds) prof[0] = __builtin_amdgcn_s_memtime();
+#endif
   Codes<kReg> codes;
   if constexpr (!kReg) codes.p = col;
   if (limit < L7M_HTTP_REC_FIXED) return L7M_VERDICT_PARSE_ERROR;
@@ -216,6 +285,7 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   if (need != w0) return L7M_VERDICT_PARSE_ERROR;
 
   if constexpr (kAblate == 2) return static_cast<int32_t>(w0 & 7u);
+  HPROF(1);
   uint64_t present = 0;
   codes.clear(h.n_dfas);
   uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
@@ -230,25 +300,32 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     present |= 1ull << kFieldMethod;
     eval_field(kFieldMethod, pos, mlen);
   }
+  HPROF(2);
   pos += mlen;
   if (flags & L7M_HTTP_F_PATH) {
     present |= 1ull << kFieldPath;
     eval_field(kFieldPath, pos, plen);
   }
+  HPROF(3);
   pos += plen;
   if (flags & L7M_HTTP_F_AUTHORITY) {
     present |= 1ull << kFieldAuthority;
     eval_field(kFieldAuthority, pos, alen);
   }
+  HPROF(4);
   pos += alen;
   if (h.has_name_dfa) {
     for (uint32_t j = 0; j < nhdr; ++j) {
       const uint32_t e = src.word(5 + j);
       const uint32_t nl = e & 0xffffu, vl = e >> 16;
-      const uint32_t code = walk_dfa(c, h.n_dfas, src, pos, nl);
       uint32_t f = kNone;
-      if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
-      else if (code) f = c.name_field[code];
+      if (h.lds_name_tab != kNone) {
+        f = name_field_of(c, h, src, pos, nl);
+      } else {
+        const uint32_t code = walk_dfa(c, h.n_dfas, src, pos, nl);
+        if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
+        else if (code) f = c.name_field[code];
+      }
       if (f != kNone && !((present >> f) & 1ull)) {  // first occurrence wins
         present |= 1ull << f;
         eval_field(f, pos + nl, vl);
@@ -257,6 +334,7 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     }
   }
 
+  HPROF(5);
   if constexpr (kAblate == 1) {
     uint32_t acc = static_cast<uint32_t>(present);
     for (uint32_t d = 0; d < h.n_dfas; ++d) acc += codes.get(d);
@@ -339,6 +417,7 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
       if (cl.len) scan(cl);
     }
   if (h.zero_list.len) scan(h.zero_list);
+  HPROF(6);
 
   if (h.allow_no_l7) return L7M_VERDICT_ALLOW_NO_L7;
   return best == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(best);
@@ -394,6 +473,10 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
   c.cr = prog + h.off_cr;
   c.remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
   uint32_t* mycol = col + tid;
+#ifdef L7M_PROF
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prof_tile = 0;
+#endif
 
   // This wave's contiguous share of the batch, consumed in tiles of <= 64
   // records.  Software pipeline per wave: while tile t is evaluated from the
@@ -463,23 +546,29 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
     const uint64_t o = t.o, onext = t.onext, base = t.base;
     const uint32_t k = t.k, take = t.take;
     int32_t v = 0;
+#ifdef L7M_PROF
+    const uint64_t te0 = __builtin_amdgcn_s_memtime();
+#endif
     if (lane < take) {
       bool done = false;
       if (lane < k && onext - o >= L7M_HTTP_REC_FIXED) {
         const LdsSrc s{reinterpret_cast<const uint32_t*>(stg + (o - base))};
         const uint32_t w0 = s.word(0);
         if (((static_cast<uint64_t>(w0) + 3) & ~3ull) <= onext - o) {
-          v = eval_record<kReg, kAblate>(c, h, s, onext - o, mycol);
+          v = eval_record<kReg, kAblate>(c, h, s, onext - o, mycol PROF_ARG);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: read HBM directly
         const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
         const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-        v = inb ? eval_record<kReg, kAblate>(c, h, s, arena_bytes - o, mycol) : L7M_VERDICT_PARSE_ERROR;
+        v = inb ? eval_record<kReg, kAblate>(c, h, s, arena_bytes - o, mycol PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
       }
       verdicts[t.cur + lane] = v;
     }
+#ifdef L7M_PROF
+    prof_tile += __builtin_amdgcn_s_memtime() - te0;
+#endif
     if (kHits != kNoHits) {
       uint32_t slot = kNone;
       if (lane < take && v != L7M_VERDICT_ALLOW_NO_L7)
@@ -493,6 +582,21 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
     wave_sync();  // the stage is overwritten by the next tile
     t = t2;
   }
+#ifdef L7M_PROF
+  if (blockIdx.x == 0 && wv == 0) {
+    prof[7] = prof_tile;
+    for (int q = 1; q < 8; ++q)
+      for (uint32_t m = 1; m < 64; m <<= 1) {
+        const uint64_t o2 = shfl64(prof[q], lane ^ m);
+        prof[q] = o2 > prof[q] ? o2 : prof[q];
+      }
+    if (lane == 0)
+      printf("L7M_PROF validate %llu method %llu path %llu authority %llu headers %llu verify %llu eval %llu\n",
+             (unsigned long long)prof[1], (unsigned long long)prof[2], (unsigned long long)prof[3],
+             (unsigned long long)prof[4], (unsigned long long)prof[5], (unsigned long long)prof[6],
+             (unsigned long long)prof[7]);
+  }
+#endif
   if (kHits == kLdsHits) {
     __syncthreads();
     for (uint32_t i = tid; i < n_ctr; i += kBlock)
@@ -524,8 +628,8 @@ static void launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t
                        unsigned long long* hits, uint32_t stage) {
   static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     attr_set = true;
   }
   hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,

@@ -119,8 +119,15 @@ struct HttpHeader {
   uint32_t lds_fields;     // name_field copies (always resident)
   uint32_t lds_name_field;
   uint32_t total_words;
-  uint32_t pad[9];         // header = 32 words
+  uint32_t lds_name_tab;   // LDS image offset of the header-name table, or kNone
+  uint32_t name_tab_mask;  // its slot count - 1 (power of two)
+  uint32_t pad[7];         // header = 32 words
 };
+// Header-name table (LDS image): exact lower-case header names of the rules
+// -> field id, open addressing on the program.h name hash; slot =
+// {hash (0 = empty), len, field, image word offset of the zero-padded name}.
+// Replaces the walk of the header-name DFA when it fits kMaxNameTabBytes.
+constexpr uint32_t kMaxNameTabBytes = 8192;
 static_assert(sizeof(HttpHeader) == 128, "header is 32 words");
 
 // ---------------------------------------------------------------- Kafka --

@@ -19,9 +19,26 @@ ES16_LATCHED = 0xFFFF
 CR_REMOTE = 0x80000000
 HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_dfa off_dfas off_fields "
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
-              "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words").split()
+              "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
+              "name_tab_mask").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask").split()
+
+
+def name_hash(data: bytes) -> int:
+    """program.h name_hash_step / name_hash_final."""
+    M = 0xFFFFFFFF
+    words = max(6, (len(data) + 3) // 4)
+    h = 0
+    for k in range(words):
+        w = int.from_bytes(data[4 * k:4 * k + 4].ljust(4, b"\0"), "little")
+        h = ((h ^ w) * 0x9E3779B1) & M
+        h ^= h >> 15
+    h = ((h ^ len(data)) * 0x85EBCA6B) & M
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M
+    h ^= h >> 16
+    return h or 1
 
 
 class HttpProgram:
@@ -43,6 +60,21 @@ class HttpProgram:
             self.dfas.append(d)
         self.fields = [tuple(self.img[h["lds_fields"] + 4 * f: h["lds_fields"] + 4 * f + 4])
                        for f in range(h["n_fields"])]
+
+    def name_tab_lookup(self, name: bytes):
+        h = self.h
+        hk = name_hash(name)
+        at = hk & h["name_tab_mask"]
+        while True:
+            sl = self.img[h["lds_name_tab"] + 4 * at: h["lds_name_tab"] + 4 * at + 4]
+            if sl[0] == 0:
+                return KNONE
+            if sl[0] == hk and sl[1] == len(name):
+                words = self.img[sl[3]: sl[3] + (len(name) + 3) // 4]
+                stored = b"".join(int(x).to_bytes(4, "little") for x in words)[:len(name)]
+                if stored == name:
+                    return sl[2]
+            at = (at + 1) & h["name_tab_mask"]
 
     def walk(self, k, data: bytes):
         """Packed double-array walk (cilium_amd/csrc/dfa_pack.h): end code."""
@@ -133,6 +165,8 @@ class HttpProgram:
                     f = 3 + (code & ~LATCHED)
                 else:
                     f = self.img[h["lds_name_field"] + code] if code else KNONE
+                if h["lds_name_tab"] != KNONE:  # the kernel's table must agree with the DFA
+                    assert self.name_tab_lookup(rec[pos:pos + nl]) == f
                 if f != KNONE and not (present >> f) & 1:
                     present |= 1 << f
                     eval_field(f, rec[pos + nl:pos + nl + vl])
