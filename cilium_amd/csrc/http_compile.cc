@@ -159,8 +159,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     return res;
   };
   if (n > 0 && !rules) return fail(L7M_EINVAL, "rules == NULL");
-  if (opts.dialect != L7M_DIALECT_ENVOY_ECMA_FULL)
-    return fail(L7M_EUNSUPPORTED, "only L7M_DIALECT_ENVOY_ECMA_FULL is implemented");
+  const bool re2 = opts.dialect == L7M_DIALECT_RE2_SEARCH;
+  if (opts.dialect != L7M_DIALECT_ENVOY_ECMA_FULL && !re2) return fail(L7M_EINVAL, "unknown dialect");
   if (n >= kNone / 2) return fail(L7M_ETOOBIG, "too many rules");
 
   // 1-2. translate, field/pattern assignment
@@ -214,6 +214,9 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
 
   // 3. parse patterns and build DFA groups per field
   re::DfaLimits lim;
+  // Unanchored-search DFAs of several patterns grow with the product of the
+  // patterns' progress states; fail group construction early and split.
+  if (re2) lim.max_states = 1u << 14;
   if (opts.max_dfa_states) lim.max_states = opts.max_dfa_states;
   if (opts.max_table_bytes) lim.max_table_bytes = opts.max_table_bytes;
   std::vector<std::vector<Group>> groups(nf);
@@ -225,7 +228,17 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     std::vector<const re::Ast*> ptrs;
     for (size_t p = 0; p < fpats[f].size(); ++p) {
       const auto& fp = fpats[f][p];
-      if (fp.kind == MatchKind::Regex) {
+      if (fp.kind == MatchKind::Regex && re2) {
+        // Go regexp.MustCompile(p).MatchString(v): RE2 syntax, unanchored.
+        std::string perr;
+        re::Status st = re::parse_re2(fp.value, &asts[p], &perr);
+        if (st == re::Status::Syntax)
+          return fail(L7M_EINVAL_REGEX, "invalid regex '" + fp.value + "' on " + field_names[f] + ": " + perr +
+                                            " (regexp.Compile would fail)");
+        if (st != re::Status::Ok)
+          return fail(L7M_EUNSUPPORTED, "regex '" + fp.value + "': " + perr + " is outside the RE2 byte subset");
+        re::make_search(&asts[p]);
+      } else if (fp.kind == MatchKind::Regex) {
         try {
           std::regex probe(fp.value, std::regex::ECMAScript | std::regex::optimize);
           (void)probe;

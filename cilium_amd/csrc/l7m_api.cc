@@ -282,7 +282,7 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
     if (doff) (void)hipFree(doff);
     if (dv) (void)hipFree(dv);
     if (dh) (void)hipFree(dh);
-    hipStreamDestroy(st);
+    (void)hipStreamDestroy(st);
   };
   // Pad the arena copy so that the kernels' aligned word loads never run past it.
   size_t abytes = (arena_bytes + 64) & ~size_t(3);
@@ -318,7 +318,7 @@ int l7m_alloc_pinned(size_t bytes, void** out) {
 }
 
 void l7m_free_pinned(void* p) {
-  if (p) hipHostFree(p);
+  if (p) (void)hipHostFree(p);
 }
 
 }  // extern "C"

@@ -42,6 +42,15 @@ struct Ast {
 // anything it cannot parse and Unsupported for non-regular constructs.
 Status parse_ecma(const std::string& pat, Ast* out, std::string* err);
 
+// Parse `pat` as Go regexp (RE2) syntax for L7M_DIALECT_RE2_SEARCH
+// (regex_re2.cc): Syntax where regexp.Compile fails, Unsupported for valid
+// RE2 outside the byte-exact subset.
+Status parse_re2(const std::string& pat, Ast* out, std::string* err);
+
+// Wrap a parsed pattern for unanchored search (regexp.MatchString):
+// [\x00-\xff]* p [\x00-\xff]*.
+void make_search(Ast* a);
+
 // AST matching exactly the bytes of `lit` (Envoy HeaderMatchType::Value).
 Ast literal_ast(const std::string& lit);
 

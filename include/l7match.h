@@ -69,7 +69,7 @@ extern "C" {
 
 /* ---- dialects ------------------------------------------------------------ */
 #define L7M_DIALECT_ENVOY_ECMA_FULL 0 /* std::regex ECMAScript, regex_match (full)  */
-#define L7M_DIALECT_RE2_SEARCH 1      /* reserved: RE2 unanchored search (not yet)  */
+#define L7M_DIALECT_RE2_SEARCH 1      /* Go regexp MatchString: RE2, unanchored     */
 
 #define L7M_PROTO_HTTP 1
 #define L7M_PROTO_KAFKA 2

@@ -4,7 +4,10 @@
 // __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.  The
 // product (libl7match.so) never links, loads or calls it.
 //
-// HTTP (dialect envoy-ecma-full):
+// HTTP (dialect envoy-ecma-full; dialect re2-search replaces regex_match by
+// std::regex_search, which equals Go regexp MatchString on the grammar and
+// inputs the RE2 tests use — printable ASCII subjects, no CR/LF, no
+// engine-specific syntax — pinned by tests/golden/re2_search.json):
 //   getHTTPRule            pkg/envoy/server.go:261-320
 //   SortHeaderMatchers     pkg/envoy/sort.go:205-250 (panic on nil Regex -> error)
 //   HeaderData / matchHeaders (Envoy @ envoy/WORKSPACE:10, called from
@@ -58,6 +61,7 @@ struct HeaderData {
   std::regex re;
 };
 struct HttpOracle {
+  bool search = false;  // L7M_DIALECT_RE2_SEARCH
   std::vector<std::vector<HeaderData>> rules;
   std::vector<std::unordered_set<uint32_t>> remotes;  // allowed_remotes_ (empty = any)
 };
@@ -129,7 +133,10 @@ int32_t eval_http_one(const HttpOracle& o, const HttpReq& q) {
           break;
         }
       if (!v) { all = false; break; }
-      if (hd.kind == 0 && !std::regex_match(*v, hd.re)) { all = false; break; }
+      if (hd.kind == 0 && !(o.search ? std::regex_search(*v, hd.re) : std::regex_match(*v, hd.re))) {
+        all = false;
+        break;
+      }
       if (hd.kind == 1 && *v != hd.value) { all = false; break; }
     }
     if (all) return static_cast<int32_t>(i);
@@ -561,8 +568,10 @@ void parallel_for(size_t n, int threads, F&& f) {
 
 extern "C" {
 
-int orc_http_new(const l7m_http_rule* rules, size_t n, void** out, char* err, size_t errlen) {
+int orc_http_new_dialect(const l7m_http_rule* rules, size_t n, uint32_t dialect, void** out, char* err,
+                         size_t errlen) {
   auto* o = new HttpOracle();
+  o->search = dialect == L7M_DIALECT_RE2_SEARCH;
   for (size_t i = 0; i < n; ++i) {
     const l7m_http_rule& r = rules[i];
     std::vector<Matcher> ms;
@@ -621,6 +630,10 @@ int orc_http_new(const l7m_http_rule* rules, size_t n, void** out, char* err, si
   return L7M_OK;
 }
 
+int orc_http_new(const l7m_http_rule* rules, size_t n, void** out, char* err, size_t errlen) {
+  return orc_http_new_dialect(rules, n, L7M_DIALECT_ENVOY_ECMA_FULL, out, err, errlen);
+}
+
 int orc_http_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint64_t* offs, size_t n,
                   int32_t* verdicts, int threads) {
   const HttpOracle& o = *static_cast<HttpOracle*>(h);
@@ -634,6 +647,15 @@ int orc_regex_match(const char* pattern, const char* input, size_t input_len) {
   try {
     std::regex re(pattern, std::regex::optimize);
     return std::regex_match(std::string(input, input_len), re) ? 1 : 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+int orc_regex_search(const char* pattern, const char* input, size_t input_len) {
+  try {
+    std::regex re(pattern, std::regex::optimize);
+    return std::regex_search(std::string(input, input_len), re) ? 1 : 0;
   } catch (...) {
     return -1;
   }

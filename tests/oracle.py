@@ -19,12 +19,15 @@ def _load():
     lib = ctypes.CDLL(ORACLE_SO)
     P, sz = ctypes.c_void_p, ctypes.c_size_t
     lib.orc_http_new.argtypes = [ctypes.POINTER(L._HttpRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.orc_http_new_dialect.argtypes = [ctypes.POINTER(L._HttpRule), sz, ctypes.c_uint32, ctypes.POINTER(P),
+                                         ctypes.c_char_p, sz]
     lib.orc_http_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_http_free.argtypes = [P]
     lib.orc_kafka_new.argtypes = [ctypes.POINTER(L._KafkaRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.orc_kafka_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_kafka_free.argtypes = [P]
     lib.orc_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
+    lib.orc_regex_search.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
     return lib
 
 
@@ -38,12 +41,12 @@ class OracleError(RuntimeError):
 
 
 class HttpOracle:
-    def __init__(self, rules):
+    def __init__(self, rules, dialect=L.DIALECT_ENVOY_ECMA_FULL):
         keep = []
         arr = (L._HttpRule * max(1, len(rules)))(*[L._http_rule_struct(r, keep) for r in rules])
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(512)
-        rc = _lib.orc_http_new(arr, len(rules), ctypes.byref(h), err, 512)
+        rc = _lib.orc_http_new_dialect(arr, len(rules), dialect, ctypes.byref(h), err, 512)
         if rc != 0:
             raise OracleError(rc, err.value.decode(errors="replace"))
         self._h = h
@@ -89,3 +92,8 @@ class KafkaOracle:
 def regex_match(pattern: str, value: bytes) -> int:
     """std::regex_match(value, std::regex(pattern, optimize)) -> 1/0, -1 if invalid."""
     return _lib.orc_regex_match(pattern.encode(), value, len(value))
+
+
+def regex_search(pattern: str, value: bytes) -> int:
+    """std::regex_search(value, std::regex(pattern, optimize)) -> 1/0, -1 if invalid."""
+    return _lib.orc_regex_search(pattern.encode(), value, len(value))

@@ -97,10 +97,10 @@ def test_invalid_regex_nacks_and_unsupported_is_explicit():
         assert e.value.code == L.L7M_EUNSUPPORTED, unsup
 
 
-def test_re2_dialect_not_yet_available():
+def test_unknown_dialect_is_rejected():
     with pytest.raises(L.L7Error) as e:
-        L.RuleSet.compile_http([L.PortRuleHTTP(Path="/a")], dialect=L.DIALECT_RE2_SEARCH)
-    assert e.value.code == L.L7M_EUNSUPPORTED
+        L.RuleSet.compile_http([L.PortRuleHTTP(Path="/a")], dialect=7)
+    assert e.value.code == L.L7M_EINVAL
 
 
 # ------------------------------------------------- oracle vs known answers --

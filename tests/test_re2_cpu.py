@@ -1,0 +1,89 @@
+"""L7M_DIALECT_RE2_SEARCH (Go regexp MatchString) on CPU: the oracle
+(std::regex_search) pinned by tests/golden/re2_search.json (Python re.search
+vectors over the intersection grammar + RE2 syntax rules; "RE2-semantics,
+not run against Go"), and the RE2 compiler checked through the program
+interpreter against the same vectors and the oracle."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from cilium_amd import l7match as L
+from oracle import HttpOracle, regex_search
+from program_interp import HttpProgram
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "re2_search.json")
+RE2 = L.DIALECT_RE2_SEARCH
+
+
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def _by_pattern(cases):
+    out = {}
+    for c in cases:
+        out.setdefault(c["pattern"], []).append((c["subject"].encode("latin-1"), c["match"]))
+    return out
+
+
+def test_oracle_pinned_by_golden_vectors():
+    for c in golden()["search"]:
+        assert regex_search(c["pattern"], c["subject"].encode("latin-1")) == int(c["match"]), c
+
+
+def _interp_paths(pattern, subjects):
+    rs = L.RuleSet.compile_http([L.PortRuleHTTP(Path=pattern)], dialect=RE2)
+    arena, offs = L.pack_http([L.HTTPRequest("GET", s, "h") for s in subjects])
+    return HttpProgram(rs.program()).eval(arena, offs)
+
+
+def test_compiler_matches_golden_search_vectors():
+    for pattern, items in _by_pattern(golden()["search"]).items():
+        got = _interp_paths(pattern, [s for s, _ in items])
+        assert [int(v) == 0 for v in got] == [m for _, m in items], pattern
+
+
+def test_syntax_rules():
+    for c in golden()["syntax"]:
+        st = c["status"]
+        if st == "ok":
+            got = _interp_paths(c["pattern"], [c["subject"].encode("latin-1")])
+            assert (int(got[0]) == 0) == c["match"], c
+            continue
+        with pytest.raises(L.L7Error) as e:
+            L.RuleSet.compile_http([L.PortRuleHTTP(Path=c["pattern"])], dialect=RE2)
+        want = {"invalid": [L.L7M_EINVAL_REGEX], "unsupported": [L.L7M_EUNSUPPORTED],
+                "invalid_or_unsupported": [L.L7M_EINVAL_REGEX, L.L7M_EUNSUPPORTED]}[st]
+        assert e.value.code in want, c
+
+
+def test_search_differs_from_full_match():
+    rules = [L.PortRuleHTTP(Path="/public/.*")]
+    arena, offs = L.pack_http([L.HTTPRequest("GET", "/x/public/a", "h")])
+    assert HttpProgram(L.RuleSet.compile_http(rules).program()).eval(arena, offs).tolist() == [-1]
+    assert HttpProgram(L.RuleSet.compile_http(rules, dialect=RE2).program()).eval(arena, offs).tolist() == [0]
+
+
+def test_multi_rule_first_match_vs_oracle():
+    rng = np.random.default_rng(21)
+    cases = golden()["search"]
+    pats = sorted({c["pattern"] for c in cases})
+    rules = []
+    for i in range(60):
+        rules.append(L.PortRuleHTTP(Path=str(rng.choice(pats)),
+                                    Method=str(rng.choice(["", "GET", "^(GET|HEAD)$", "P"])),
+                                    Host=str(rng.choice(["", "svc", "\\.local$"])),
+                                    Headers=["x-t: v1"] if rng.random() < 0.2 else []))
+    subjects = [c["subject"] for c in cases]
+    reqs = [L.HTTPRequest(str(rng.choice(["GET", "POST", "HEAD", "PUT"])), str(rng.choice(subjects)),
+                          str(rng.choice(["svc1.ns.local", "a.local", "example.com"])),
+                          [("x-t", "v1")] if rng.random() < 0.5 else [])
+            for _ in range(1500)]
+    arena, offs = L.pack_http(reqs)
+    got = HttpProgram(L.RuleSet.compile_http(rules, dialect=RE2).program()).eval(arena, offs)
+    exp = HttpOracle(rules, dialect=RE2).eval(arena, offs)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
