@@ -147,6 +147,62 @@ Req http_req_cfg2(const std::vector<HttpRuleT>& rules, uint64_t seed, uint64_t i
   return q;
 }
 
+// ------------------------------------------------------ adversarial (5) --
+// NFA-heavy path families and long header values.
+//   i % 5 == 0: /a{i}/(a|aa)*b            (alternation blow-up for backtrackers)
+//   i % 5 == 1: /x{i}/.*(x|y).*(z|w).*q    (wildcards)
+//   i % 5 == 2: /l{i}/(w0|...|w99)          (100-way literal alternation)
+//   i % 5 == 3: /c{i}/[a-z]*[a-z]*[a-z]*[a-z]*z
+//   i % 5 == 4: /f{i}/(.{0,8}){1,8}foo      (counted-repeat blow-up)
+// Every 97th rule also requires the literal header x-blob: <1 KiB value>.
+std::string adv_word(uint32_t i, uint32_t k) {
+  Rng r(mix(0x574f5244ull ^ i, k));
+  return word(r, 3, 8);
+}
+std::string adv_blob(uint32_t i, uint32_t len) {
+  Rng r(mix(0x424c4f42ull, i));
+  return word(r, len, len, "abcdefghijklmnopqrstuvwxyz0123456789-_.");
+}
+std::string adv_path_rule(uint32_t i) {
+  const std::string id = std::to_string(i);
+  switch (i % 5) {
+    case 0: return "/a" + id + "/(a|aa)*b";
+    case 1: return "/x" + id + "/.*(x|y).*(z|w).*q";
+    case 2: {
+      std::string alt;
+      for (uint32_t k = 0; k < 100; ++k) alt += (k ? "|" : "") + adv_word(i, k);
+      return "/l" + id + "/(" + alt + ")";
+    }
+    case 3: return "/c" + id + "/[a-z]*[a-z]*[a-z]*[a-z]*z";
+    default: return "/f" + id + "/(.{0,8}){1,8}foo";
+  }
+}
+Req http_req_cfg5(uint64_t seed, uint32_t n_rules, uint64_t i) {
+  Rng r(mix(seed, i));
+  const uint32_t ri = r.u(n_rules);
+  const std::string id = std::to_string(ri);
+  const bool good = r.p(0.5);
+  Req q;
+  q.method = "GET";
+  switch (ri % 5) {
+    case 0: q.path = "/a" + id + "/" + std::string(r.u(21), 'a') + (good ? "b" : "c"); break;
+    case 1: q.path = "/x" + id + "/" + word(r, 0, 30, "xyzwq.") + (good ? "q" : "."); break;
+    case 2: q.path = "/l" + id + "/" + (good ? adv_word(ri, r.u(100)) : word(r, 3, 8)); break;
+    case 3: q.path = "/c" + id + "/" + word(r, 0, 20) + (good ? "z" : "y"); break;
+    default: q.path = "/f" + id + "/" + word(r, 0, 70, "abfo.") + (good ? "foo" : "fob"); break;
+  }
+  q.authority = "adv.example";
+  fillers(r, q);
+  if (ri % 97 == 0 && r.p(0.8)) {
+    std::string b = adv_blob(ri, 1024);
+    if (!r.p(0.7)) b[r.u(1024)] = '#';
+    q.hdrs.push_back({"x-blob", b});
+  } else if (r.p(0.03)) {
+    q.hdrs.push_back({"x-blob", adv_blob(static_cast<uint32_t>(i), 1024 + r.u(65535 - 1024))});
+  }
+  return q;
+}
+
 size_t pack(const Req& q, uint8_t* out, uint32_t remote, uint16_t dport) {
   std::vector<const char*> n, v;
   for (auto& h : q.hdrs) {
@@ -314,6 +370,12 @@ const char* l7g_rules_text(int config, uint64_t seed, uint32_t n_rules) {
       std::string hdr = t.hdr == 1 ? "x-tenant: t" + std::to_string(i % 17) : t.hdr == 2 ? "x-debug" : "";
       g_text += path + "\t" + kMethods[t.method] + "\t" + host + "\t" + hdr + "\n";
     }
+  } else if (config == 5) {
+    for (uint32_t i = 0; i < n_rules; ++i) {
+      g_text += adv_path_rule(i) + "\tGET\t\t";
+      if (i % 97 == 0) g_text += "x-blob: " + adv_blob(i, 1024);
+      g_text += "\n";
+    }
   } else if (config == 3) {
     auto rules = kafka_rules_cfg3(seed, n_rules);
     for (uint32_t i = 0; i < n_rules; ++i) {
@@ -338,6 +400,7 @@ uint64_t l7g_requests(int config, uint64_t seed, uint32_t n_rules, uint64_t star
   auto gen_one = [&](uint64_t i, uint8_t* out) -> size_t {
     if (config == 1) return pack(http_req_cfg1(seed, i), out, 1, 80);
     if (config == 2) return pack(http_req_cfg2(h2, seed, i), out, 1, 80);
+    if (config == 5) return pack(http_req_cfg5(seed, n_rules, i), out, 1, 80);
     auto w = kafka_req_cfg3(seed, i);
     size_t padded = (w.size() + 3) & ~size_t(3);
     if (out) {

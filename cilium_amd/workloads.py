@@ -17,6 +17,7 @@ CONFIGS = {
     1: dict(name="readme-http-1rule", seed=0xC1, n_rules=1, n_requests=1_000_000, proto=L.PROTO_HTTP),
     2: dict(name="http-1k-rules", seed=0xC2, n_rules=1000, n_requests=64_000_000, proto=L.PROTO_HTTP),
     3: dict(name="kafka-10k-rules", seed=0xC3, n_rules=10000, n_requests=64_000_000, proto=L.PROTO_KAFKA),
+    5: dict(name="adversarial-100k-rules", seed=0xC5, n_rules=100_000, n_requests=1_000_000, proto=L.PROTO_HTTP),
 }
 
 
