@@ -100,6 +100,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = args.config
+    if cfg == 4:
+        return run_mixed(args, world, rank, dev)
     c = W.CONFIGS[cfg]
     per_gpu = args.requests or c["n_requests"]
     threads = args.threads or max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
@@ -203,6 +205,129 @@ def main():
             log("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds, threads)
         print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_mixed(args, world, rank, dev):
+    """Config 4: 5k HTTP + 5k Kafka rules, 128M requests in total split by
+    protocol tag (W.mixed_parts), STRONG scaling: each rank evaluates
+    1/world of each protocol's requests.  Per step the two kernels run
+    concurrently on two HIP streams, then one RCCL all-reduce sums the
+    concatenated (R_http+2) + (R_kafka+2) counters."""
+    c = W.CONFIGS[4]
+    threads = args.threads or max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    total = args.requests * world if args.requests else c["n_requests"]
+    parts = []
+    for proto, gcfg, seed, n_rules in W.mixed_parts(4):
+        n_all = total // 2
+        lo, hi = D.shard_bounds(n_all, world, rank)
+        rules = W.rules(gcfg, seed=seed, n_rules=n_rules)
+        rs = (L.RuleSet.compile_http(rules, lds_budget_bytes=args.lds_budget) if proto == L.PROTO_HTTP
+              else L.RuleSet.compile_kafka(rules))
+        arena, offs = W.requests(gcfg, lo, hi - lo, seed=seed, n_rules=n_rules, threads=threads)
+        d_arena = torch.from_numpy(arena).to(dev)
+        d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
+        parts.append(dict(proto=proto, gcfg=gcfg, rules=rules, rs=rs, n=hi - lo, seed=seed,
+                          arena_nbytes=arena.nbytes, rec_bytes=arena.nbytes - 64, d_arena=d_arena,
+                          d_offs=d_offs, d_verd=torch.empty(hi - lo, dtype=torch.int32, device=dev),
+                          stream=torch.cuda.Stream(device=dev)))
+        del arena, offs
+        log(f"rank {rank}: part config {gcfg}: {len(rules)} rules, {hi - lo} requests")
+    n_cnt = [p["rs"].n_counters for p in parts]
+    d_hits = torch.zeros(sum(n_cnt), dtype=torch.int64, device=dev)
+    hit_views = [d_hits[:n_cnt[0]], d_hits[n_cnt[0]:]]
+    main_s = torch.cuda.current_stream()
+
+    def step(ev=None):
+        d_hits.zero_()
+        start = torch.cuda.Event(enable_timing=True)
+        start.record(main_s)
+        ends = []
+        for p, hv in zip(parts, hit_views):
+            p["stream"].wait_event(start)
+            p["rs"].eval_device(p["d_arena"], p["arena_nbytes"], p["d_offs"], p["n"], p["d_verd"],
+                                None if args.no_hits else hv,
+                                p["stream"].cuda_stream, 0)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(p["stream"])
+            main_s.wait_event(e)
+            ends.append(e)
+        D.allreduce_counters(d_hits)
+        if ev is not None:
+            ev.append((start, ends))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(evs)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [max(s.elapsed_time(e) for e in ends) for s, ends in evs]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    n_rank = sum(p["n"] for p in parts)
+    n_job = torch.tensor([n_rank], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(n_job)
+    n_job = int(n_job.item())
+    kavg = float(np.mean(kernel_ms)) / 1e3
+    alg_bytes = sum(p["rec_bytes"] + 12 * p["n"] for p in parts) + 8 * sum(n_cnt)
+    achieved = alg_bytes / kavg / 1e9
+    counters_ok = None if args.no_hits else int(d_hits.sum().item()) == n_job
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    res = {
+        "metric": f"L7 verdicts/sec ({c['name']}) + achieved HBM GB/s vs peak",
+        "value": n_job * args.steps / elapsed,
+        "unit": "verdicts/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (deterministic generator libl7gen.so, SURVEY.md §8(d))",
+        "config": {"workload": c["name"], "baseline_config": 4, "n_rules": sum(len(p["rules"]) for p in parts),
+                   "requests_total": n_job, "seed": hex(c["seed"]),
+                   "parts": [{"generator_config": p["gcfg"], "n_rules": len(p["rules"]), "requests_rank0": p["n"],
+                              "mean_record_bytes": p["rec_bytes"] / max(1, p["n"])} for p in parts],
+                   "parallelism": f"dp{world} (request-sharded per protocol, two HIP streams, "
+                                  f"RCCL all-reduce of {sum(n_cnt)} counters)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_launch": alg_bytes,
+                     "note": "both kernels, first start to last end, rank 0"},
+        "counters_ok": counters_ok,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle import HttpOracle, KafkaOracle  # test infrastructure: cpu_baseline leg only
+        n_tot, t_tot, samples = 0, 0.0, []
+        for p in parts:
+            orc = HttpOracle(p["rules"]) if p["proto"] == L.PROTO_HTTP else KafkaOracle(p["rules"])
+            a, o = W.requests(p["gcfg"], 10_000_000, 5_000, seed=p["seed"], n_rules=len(p["rules"]),
+                              threads=threads)
+            t1 = time.perf_counter()
+            orc.eval(a, o, threads=threads)
+            rate = 5_000 / max(1e-6, time.perf_counter() - t1)
+            n = int(min(20_000_000, max(5_000, rate * args.cpu_baseline_seconds / 2)))
+            a, o = W.requests(p["gcfg"], 20_000_000, n, seed=p["seed"], n_rules=len(p["rules"]), threads=threads)
+            t1 = time.perf_counter()
+            orc.eval(a, o, threads=threads)
+            dt = time.perf_counter() - t1
+            n_tot, t_tot = n_tot + n, t_tot + dt
+            samples.append(f"{n} requests of part config {p['gcfg']} in {dt:.1f} s")
+        res["cpu_baseline"] = {"value": n_tot / t_tot, "unit": "verdicts/s", "cores": threads, "kind": "port",
+                               "sample": "; ".join(samples) + f" (oracle/l7oracle.cc on {threads} threads)"}
+    print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -437,7 +437,10 @@ __device__ __forceinline__ void wave_sync() {
 // Per-rule hit counters: none, per-workgroup LDS counters flushed once at the
 // end (small rule sets), or wave-aggregated global atomics.
 enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
-constexpr uint32_t kMaxLdsCounters = 4096;
+#ifndef L7M_MAX_LDS_COUNTERS
+#define L7M_MAX_LDS_COUNTERS 8192
+#endif
+constexpr uint32_t kMaxLdsCounters = L7M_MAX_LDS_COUNTERS;
 
 template <int kHits, bool kReg, int kAblate>
 __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,

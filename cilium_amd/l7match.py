@@ -304,11 +304,11 @@ class RuleSet:
         _lib.l7m_ruleset_get_info(self._h, ctypes.byref(info))
         self.info = info
 
-    def __del__(self):
+    def __del__(self, _release=_lib.l7m_release):  # bound early: module globals are gone at exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            _lib.l7m_release(h)
-            self._h = ctypes.c_void_p(0)
+            _release(h)
+            self._h = None
 
     @property
     def handle(self) -> ctypes.c_void_p:

@@ -17,6 +17,11 @@ CONFIGS = {
     1: dict(name="readme-http-1rule", seed=0xC1, n_rules=1, n_requests=1_000_000, proto=L.PROTO_HTTP),
     2: dict(name="http-1k-rules", seed=0xC2, n_rules=1000, n_requests=64_000_000, proto=L.PROTO_HTTP),
     3: dict(name="kafka-10k-rules", seed=0xC3, n_rules=10000, n_requests=64_000_000, proto=L.PROTO_KAFKA),
+    # Config 4 is two generators under one seed: 5k config-2 HTTP rules + 5k
+    # config-3 Kafka rules, 128M requests in total (half per protocol), see
+    # mixed_parts().  SURVEY.md §8(d) config 4.
+    4: dict(name="mixed-http-kafka-10k-rules", seed=0xC4, n_rules=10_000, n_requests=128_000_000, proto=None,
+            parts=((2, 5000), (3, 5000))),
     5: dict(name="adversarial-100k-rules", seed=0xC5, n_rules=100_000, n_requests=1_000_000, proto=L.PROTO_HTTP),
 }
 
@@ -70,3 +75,16 @@ def requests(config: int, start: int, count: int, seed: int = None, n_rules: int
                              offs.ctypes.data, threads)
     assert used == size
     return arena[: size + 64] if out_arena is None else arena, offs
+
+
+def mixed_parts(config: int = 4):
+    """Config 4 split by protocol tag: [(proto, generator config, seed, n_rules)].
+
+    In Cilium the two protocols never share a call site — HTTP verdicts are
+    taken in Envoy's filter (envoy/cilium_l7policy.cc), Kafka verdicts in the
+    Go proxy (pkg/proxy/kafka.go) — so a mixed batch is demultiplexed by its
+    protocol tag into one arena per protocol, each evaluated against its own
+    compiled rule set; request i of part p is request i of generator
+    config p under the mixed workload's seed."""
+    c = CONFIGS[config]
+    return [(CONFIGS[g]["proto"], g, c["seed"], n) for g, n in c["parts"]]
