@@ -493,10 +493,16 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     const PackedDfa& d = *all[k].d;
     const uint64_t half = (d.n_slots + 1) / 2;
     const uint64_t need = ((d.n_slots + 3) & ~3ull) + 2 * ((half + 3) & ~3ull);
-    if (img + need > budget || d.sets.size() >= kEs16Latched || all[k].npats >= kEs16Latched) continue;
-    dd[k].lds_table = img_take(d.n_slots);
-    dd[k].lds_es = 2 * img_take(half);
-    dd[k].lds_latch = 2 * img_take(half);
+    const bool es16 = d.sets.size() < kEs16Latched && all[k].npats < kEs16Latched;
+    if (es16 && img + need <= budget) {
+      dd[k].lds_table = img_take(d.n_slots);
+      dd[k].lds_es = 2 * img_take(half);
+      dd[k].lds_latch = 2 * img_take(half);
+    } else if (img + ((d.n_slots + 3) & ~3ull) <= budget) {
+      // the slot table (read once per byte) alone; end codes / latches (read
+      // once per walk) stay in the program
+      dd[k].lds_table = img_take(d.n_slots);
+    }
   }
   // Candidate tables are read once per request (after the walks), so they
   // only go to LDS while the image stays small: record staging space is worth
@@ -579,7 +585,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     if (!ce.empty()) std::memcpy(P + dd[k].ct_off, ce.data(), ce.size() * sizeof(CandEntry));
     if (dd[k].lds_table != kNone) {
       std::memcpy(I + dd[k].lds_table, d.table.data(), d.n_slots * 4ull);
-      for (uint32_t s = 0; s < d.n_slots; ++s) {
+      for (uint32_t s = 0; dd[k].lds_es != kNone && s < d.n_slots; ++s) {
         I16[dd[k].lds_es + s] = d.es[s] == kLatchedAccept ? static_cast<uint16_t>(kEs16Latched)
                                                            : static_cast<uint16_t>(d.es[s]);
         I16[dd[k].lds_latch + s] = d.latch[s] == kNone ? static_cast<uint16_t>(kEs16Latched)

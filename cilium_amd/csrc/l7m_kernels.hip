@@ -59,7 +59,7 @@ template <bool kLdsTab>
 __device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
                                              const DfaDesc& dd, uint32_t base, uint32_t last) {
   if (!base) return 0;
-  if (kLdsTab) {
+  if (kLdsTab && dd.lds_es != kNone) {  // else: slot table in LDS, end codes in the program
     const uint16_t* I16 = reinterpret_cast<const uint16_t*>(img);
     const uint32_t es = I16[dd.lds_es + base];
     if (es != kEs16Latched) return es;

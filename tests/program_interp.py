@@ -93,7 +93,7 @@ class HttpProgram:
             base = e >> 16 if (e & 0xFFFF) == base else 0
         if not base:
             return 0
-        if lds:
+        if lds and d["lds_es"] != KNONE:  # table-only LDS placement keeps end codes in the program
             es = self.img16[d["lds_es"] + base]
             if es != ES16_LATCHED:
                 return es

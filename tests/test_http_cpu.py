@@ -214,3 +214,14 @@ def test_regex_compiler_differential_fuzz():
     out = subprocess.run(["timeout", "240", exe, "7", "600", "120"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout[-3000:]
     assert "mismatches=0" in out.stdout
+
+
+def test_compiler_table_only_lds_placement_matches_oracle():
+    """A slot table that fits the LDS budget only without its u16 end codes /
+    latches is placed alone (end codes stay in the program)."""
+    rules = W.rules(2, n_rules=400)
+    arena, offs = W.requests(2, 0, 1500, n_rules=400)
+    rs = L.RuleSet.compile_http(rules, lds_budget_bytes=12288)
+    P = HttpProgram(rs.program())
+    assert any(d["lds_table"] != 0xFFFFFFFF and d["lds_es"] == 0xFFFFFFFF for d in P.dfas)
+    assert (P.eval(arena, offs) == HttpOracle(rules).eval(arena, offs)).all()

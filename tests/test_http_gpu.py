@@ -175,3 +175,19 @@ def test_eval_device_matches_host_eval_and_shards(gpu):
     a2, o2 = W.requests(2, 150_000, 150_000)
     v = np.concatenate([rs.eval(a1, o1), rs.eval(a2, o2)])
     assert (v == host_v).all()
+
+
+@pytest.mark.parametrize("budget", [1, 8192, 12288, 16384])
+def test_lds_placement_variants_parity(gpu, budget):
+    """Every LDS placement of the DFA tables — none, full (table + u16 end
+    codes), and table-only (end codes read from the program) — gives the
+    oracle's verdicts and counters."""
+    rules = W.rules(2, n_rules=400)
+    arena, offs = W.requests(2, 3_000_000, 20_000, n_rules=400)
+    rs = L.RuleSet.compile_http(rules, lds_budget_bytes=budget)
+    h = np.zeros(rs.n_counters, dtype=np.uint64)
+    got = rs.eval(arena, offs, h)
+    exp = HttpOracle(rules).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+    assert int(h.sum()) == len(offs)
