@@ -10,5 +10,5 @@ rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 420 python -u bench.py --config 4 > $OUT/bench.out 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o run --output-format csv -- \
-  python3 -u bench.py --config 4 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.out 2> $OUT/prof.err
+  python3 -u bench.py --config 4 --steps 20 --warmup 2 --no-cpu-baseline > $OUT/prof.out 2> $OUT/prof.err
 rc=$?; echo "rocprof rc=$rc"; exit $rc

@@ -17,8 +17,8 @@ step pytest_gpu 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeo
 rc=$?; [ $rc -le 1 ] || exit $rc
 step bench_http 420 python -u bench.py || exit 1
 step bench_kafka 420 python -u bench.py --config 3 || exit 1
-step prof_http 420 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_http -o run --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit 1
-step prof_kafka 420 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_kafka -o run --output-format csv -- python3 -u bench.py --config 3 --steps 3 --warmup 1 --no-cpu-baseline || exit 1
+step prof_http 420 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_http -o run --output-format csv -- python3 -u bench.py --steps 20 --warmup 2 --no-cpu-baseline || exit 1
+step prof_kafka 420 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_kafka -o run --output-format csv -- python3 -u bench.py --config 3 --steps 20 --warmup 2 --no-cpu-baseline || exit 1
 for c in FETCH_SIZE WRITE_SIZE; do
   for cfg in 2 3; do
     step pmc_${c}_$cfg 180 rocprofv3 --pmc $c -d $PWD/$OUT/pmc_${c}_$cfg -o run --output-format csv -- python3 -u bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline || exit 1
