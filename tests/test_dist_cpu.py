@@ -80,3 +80,49 @@ def test_counters_from_verdicts_semantics():
     c = D.counters_from_verdicts(v, 3)
     assert c.tolist() == [1, 2, 1, 0, 2]
     assert D.shard_bounds(10, 3, 0) == (0, 3) and D.shard_bounds(10, 3, 2) == (6, 10)
+
+
+def _mixed_worker(rank, world, port, n_all, out_dir):
+    """Config 4 as bench.run_mixed does it: per protocol part, this rank's
+    1/world of the part's requests; counters of both parts concatenated into
+    ONE buffer, one all-reduce."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    from oracle import HttpOracle, KafkaOracle
+    from cilium_amd import l7match as L
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctrs = []
+    for proto, gcfg, seed, n_rules in W.mixed_parts(4):
+        rules = W.rules(gcfg, seed=seed, n_rules=n_rules)
+        lo, hi = D.shard_bounds(n_all, world, rank)
+        arena, offs = W.requests(gcfg, lo, hi - lo, seed=seed, n_rules=n_rules, threads=1)
+        orc = HttpOracle(rules) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+        ctrs.append(D.counters_from_verdicts(orc.eval(arena, offs), len(rules)).view(np.int64))
+    ctr = torch.from_numpy(np.concatenate(ctrs))
+    D.allreduce_counters(ctr)
+    np.save(os.path.join(out_dir, f"mixed{rank}.npy"), ctr.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_mixed_config4_counters(tmp_path):
+    from oracle import HttpOracle, KafkaOracle
+    from cilium_amd import l7match as L
+    n_all = 800
+    mp.start_processes(_mixed_worker, args=(2, _free_port(), n_all, str(tmp_path)), nprocs=2,
+                       start_method="spawn", join=True)
+    full = []
+    for proto, gcfg, seed, n_rules in W.mixed_parts(4):
+        rules = W.rules(gcfg, seed=seed, n_rules=n_rules)
+        arena, offs = W.requests(gcfg, 0, n_all, seed=seed, n_rules=n_rules)
+        orc = HttpOracle(rules) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+        full.append(D.counters_from_verdicts(orc.eval(arena, offs), len(rules)).view(np.int64))
+    full = np.concatenate(full)
+    assert int(full.sum()) == 2 * n_all
+    for r in range(2):
+        assert (np.load(tmp_path / f"mixed{r}.npy") == full).all()
