@@ -72,6 +72,10 @@ struct Group {
   PackedDfa pk;
 };
 
+// Estimate-based chunking of large pattern sets (see build_groups).
+constexpr size_t kChunkMinPatterns = 64;
+constexpr uint64_t kChunkSlotBudget = 40000;  // of the 64 K slots a packed group can address
+
 int build_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> idx,
                  const re::DfaLimits& lim, std::vector<Group>* out, std::string* err) {
   std::vector<const re::Ast*> sub;
@@ -92,6 +96,35 @@ int build_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> 
   if (idx.size() == 1) {
     *err = "a single pattern exceeds the DFA state/table limit";
     return L7M_ETOOBIG;
+  }
+  if (idx.size() > kChunkMinPatterns) {
+    // Large set that does not fit one group: instead of halving (a failed
+    // subset construction per level), pack patterns greedily by the explicit
+    // transitions of their own DFAs.  Patterns of one field usually diverge
+    // on a literal prefix, so a union's slots are close to the sum of its
+    // parts; a chunk that still fails falls back to halving.
+    std::vector<std::vector<uint32_t>> chunks(1);
+    uint64_t acc = 0;
+    for (uint32_t i : idx) {
+      re::Dfa one;
+      PackedDfa pk;
+      uint64_t w = kChunkSlotBudget;  // a pattern that fails alone gets a chunk of its own
+      if (re::build_dfa({asts[i]}, lim, &one) == re::Status::Ok && pack_dfa(one, &pk) == re::Status::Ok)
+        w = pk.n_explicit + 1;
+      if (!chunks.back().empty() && acc + w > kChunkSlotBudget) {
+        chunks.emplace_back();
+        acc = 0;
+      }
+      chunks.back().push_back(i);
+      acc += w;
+    }
+    if (chunks.size() > 1) {
+      for (auto& ch : chunks) {
+        int rc = build_groups(asts, std::move(ch), lim, out, err);
+        if (rc != L7M_OK) return rc;
+      }
+      return L7M_OK;
+    }
   }
   size_t h = idx.size() / 2;
   std::vector<uint32_t> a(idx.begin(), idx.begin() + h), b(idx.begin() + h, idx.end());

@@ -22,3 +22,16 @@ def test_adversarial_compiler_vs_oracle():
     bad = np.nonzero(got != exp)[0]
     assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
     assert (exp >= 0).any() and (exp == -1).any()
+
+
+def test_adversarial_chunked_grouping_vs_oracle():
+    """> 64 path patterns that do not fit one DFA group: estimate-based
+    chunking (http_compile.cc build_groups) then halving; verdicts unchanged."""
+    rules = W.rules(5, n_rules=160)
+    arena, offs = W.requests(5, 0, 50, n_rules=160)
+    rs = L.RuleSet.compile_http(rules)
+    assert rs.info.n_dfas > 10
+    got = HttpProgram(rs.program()).eval(arena, offs)
+    exp = HttpOracle(rules).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]

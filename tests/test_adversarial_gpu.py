@@ -24,3 +24,14 @@ def test_adversarial_parity(gpu):
     bad = np.nonzero(got != exp)[0]
     assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
     assert int(h.sum()) == len(offs)
+
+
+def test_adversarial_chunked_grouping_parity(gpu):
+    rules = W.rules(5, n_rules=160)
+    arena, offs = W.requests(5, 0, 3000, n_rules=160)
+    rs = L.RuleSet.compile_http(rules)
+    assert rs.info.n_dfas > 10
+    got = rs.eval(arena, offs)
+    exp = HttpOracle(rules).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
