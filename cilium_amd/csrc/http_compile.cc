@@ -487,7 +487,18 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   // ---- LDS image: descriptors always; then, hottest DFA first (header
   // names, path, authority, method, header values), slot table + u16 end
   // codes/latches; then candidate tables and set masks, within the budget.
-  const uint64_t budget = (opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget) / 4;
+  uint64_t budget_bytes = opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget;
+  {
+    // The kernel's LDS also holds the per-lane end-code columns (> 8 value
+    // DFAs: 4 bytes x 1024 lanes each), the hit counters and >= 2 KiB of
+    // record stage per wave: shrink the image so many-group rule sets still
+    // launch (their tables are then walked from L2 / HBM).
+    const uint64_t codes = ndfa > kLdsRegDfas ? 4096ull * ndfa : 0;
+    const uint64_t ctr = 4ull * (n + 2);
+    const uint64_t fixed = codes + ctr + kLdsMinStageTotal;
+    budget_bytes = std::min<uint64_t>(budget_bytes, fixed < kLdsTotal ? kLdsTotal - fixed : 0);
+  }
+  const uint64_t budget = budget_bytes / 4;
   uint64_t img = 0;  // image words
   auto img_take = [&](uint64_t words) {
     uint64_t o = img;

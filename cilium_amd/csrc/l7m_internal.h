@@ -28,6 +28,10 @@ inline uint32_t name_hash(const std::string& s) {
 
 constexpr uint32_t kDefaultLdsBudget = 48u * 1024u;  // bytes of DFA tables in the LDS image
 constexpr uint32_t kLdsCtBudget = 24u * 1024u;       // ... including candidate tables
+// HTTP kernel LDS facts the compiler sizes the image against (l7m_kernels.hip)
+constexpr uint64_t kLdsTotal = 160u * 1024u;         // gfx950 LDS per CU (one workgroup)
+constexpr uint32_t kLdsRegDfas = 8;                  // <= 8 value DFAs: end codes in registers
+constexpr uint64_t kLdsMinStageTotal = 16u * (2048u + 16u);  // 16 waves x 2 KiB stage
 
 // One getHTTPRule HeaderMatcher (pkg/envoy/server.go:261-320).
 struct HeaderMatcher {
