@@ -1,27 +1,35 @@
-// dfa_pack.h — pack a multi-pattern DFA into the GPU's byte-indexed
-// double-array form ("DA table") with single-pattern tail sharing.
+// dfa_pack.h — the GPU's packed multi-pattern automaton ("DA table") and the
+// scalable builder that produces it for one header field.
 //
-// Why: a dense (states x classes) table for 1k realistic rules is megabytes
-// (every pattern owns a private copy of shared tails such as
-// `/v[0-9]+/(users|orders|items)/[0-9]+`, and trie-like prefix states are
-// almost all dead entries), so every DFA step would be a random L2 access.
-// The packed form below is 10-100x smaller and usually fits gfx950's LDS,
-// and a step is ONE dependent 4-byte LDS read indexed by the raw input byte
-// (no byte-class lookup on the critical path):
+// Packed form (one u32 slot table T per field automaton):
 //
 //     e = T[base + byte];
-//     base = (e & 0xffff) == base ? e >> 16 : 0;     // base 0 = dead state
+//     base = (e & 0xff) == byte ? e >> 8 : 0;          // base 0 = dead state
 //
-// Every non-dead transition is an explicit slot whose check half holds the
-// owner's base; a slot another state owns (or an empty one, check 0xffff)
-// means "dead".  The dead state owns no slot, so it is absorbing.
+// Every non-dead transition is an explicit slot holding the target's base
+// (24 bits) and the input byte it was placed for (8 bits).  Bases are unique
+// per state, so slot s can only be "base + byte" for the state whose base is
+// s - label: the byte label is a complete ownership check (no owner field).
+// An empty slot is 0 (next base 0 = dead whatever its label).  One step is
+// ONE dependent 4-byte read indexed by the raw input byte; 24-bit bases
+// address 16 M slots, so a whole field (100k rules) is one automaton.
 //
 // Tail sharing ("latching"): a state from which exactly one pattern can still
-// match is "latched".  Latched states are minimised with binary acceptance,
-// so all patterns whose residual languages coincide share ONE copy of the
-// tail; the pattern identity is recovered from the slot of the transition
-// that entered the latched region (LATCH[slot]), or from start_latch when the
-// start state itself is latched.  All latched states have base >= region.
+// match is "latched".  Latched states are the residual automata of the
+// patterns, shared by every pattern with the same residual (config 2: the
+// 500 `/svc{i}/v[0-9]+/(users|orders|items)/[0-9]+` rules share one tail;
+// config 5: the 20k `(.{0,8}){1,8}foo` rules share one), so the pattern
+// identity is recovered from the slot of the transition that entered the
+// latched region (latch[slot]) or from start_latch when the start state itself
+// is latched.  All latched states have base >= region.
+//
+// Builder (build_field_dfa): each pattern is split into a literal prefix and a
+// residual regex; distinct residuals are determinised once (regex_ecma.h
+// build_dfa); the multi-pattern part is the product of the per-pattern DFAs
+// over a field-wide byte partition, computed only until a single pattern
+// remains live (for literal-prefixed rule sets it is the prefix trie).  Cost
+// is linear in the rules for prefix-diverging sets instead of a subset
+// construction over the union NFA.
 #pragma once
 #include <cstdint>
 #include <vector>
@@ -31,26 +39,40 @@
 namespace l7m {
 
 constexpr uint32_t kLatchedAccept = 0x80000000u;  // end code: accept the latched pattern
-constexpr uint32_t kMaxDaBase = 65535 - 256;      // 16-bit bases and slots
+constexpr uint32_t kMaxDaBase = (1u << 24) - 1 - 256;  // 24-bit bases and slots
 
 struct PackedDfa {
   uint32_t n_slots = 0;          // table length incl. 256 slots of tail padding
-  std::vector<uint32_t> table;   // check | next_base << 16; empty slot check = 0xffff
+  std::vector<uint32_t> table;   // next_base << 8 | byte label; empty slot 0
   std::vector<uint32_t> es;      // per base: 0 no match, set id (index into sets), or kLatchedAccept
-  std::vector<uint32_t> latch;   // per slot: pattern entered by that transition (0xffffffff none)
+  std::vector<uint32_t> latch;   // per slot < region + 256: pattern entered by that transition (0xffffffff none)
   uint32_t start_base = 0;       // 0 = dead start (nothing can match)
   uint32_t region = 1;           // bases >= region are latched states
   uint32_t start_latch = 0xffffffffu;
   uint32_t nstates = 0;          // packed states incl. dead
-  uint32_t n_explicit = 0;       // explicit transitions
+  uint64_t n_explicit = 0;       // explicit transitions
+  uint32_t n_multi = 0;          // multi-pattern (product) states
+  uint32_t n_residuals = 0;      // distinct residual automata
   std::vector<std::vector<uint32_t>> sets;  // end sets (set id -> sorted pattern ids), set 0 empty
 };
 
-// Returns Ok, or TooBig when a slot would exceed 16 bits (caller splits).
-re::Status pack_dfa(const re::Dfa& d, PackedDfa* out);
+struct FieldDfaLimits {
+  size_t max_multi_states = 1u << 21;  // product states before the caller splits the pattern set
+  uint64_t max_slots = kMaxDaBase;     // packed bases
+};
+
+// Build the packed automaton of patterns[0..n) (pattern id = index).
+// Returns Ok, TooBig (a limit was exceeded: the caller splits the set) or
+// the first residual's build_dfa error.
+re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const FieldDfaLimits& lim,
+                           PackedDfa* out);
 
 // Reference walk of a packed DFA on the host (tests / interpreter parity):
 // returns the end code (0, set id, or kLatchedAccept | pattern).
 uint32_t packed_walk(const PackedDfa& p, const uint8_t* s, size_t n);
+
+// Explicit-transition estimate of one pattern (its literal prefix plus its
+// residual automaton), used to chunk huge pattern sets before building.
+uint64_t pattern_slot_estimate(const re::Ast& a);
 
 }  // namespace l7m

@@ -72,18 +72,16 @@ struct Group {
   PackedDfa pk;
 };
 
-// Estimate-based chunking of large pattern sets (see build_groups).
-constexpr size_t kChunkMinPatterns = 64;
-constexpr uint64_t kChunkSlotBudget = 40000;  // of the 64 K slots a packed group can address
-
+// Build the field automata of one field's patterns: normally ONE automaton
+// (dfa_pack.h, linear in the rules for prefix-diverging sets); a set whose
+// product exceeds the limits (e.g. unanchored RE2-search patterns, which never
+// latch) is split in halves.
 int build_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> idx,
-                 const re::DfaLimits& lim, std::vector<Group>* out, std::string* err) {
+                 const FieldDfaLimits& lim, std::vector<Group>* out, std::string* err) {
   std::vector<const re::Ast*> sub;
   for (uint32_t i : idx) sub.push_back(asts[i]);
   Group g;
-  re::Dfa dfa;
-  re::Status st = re::build_dfa(sub, lim, &dfa);
-  if (st == re::Status::Ok) st = pack_dfa(dfa, &g.pk);  // TooBig: > 32K packed bases
+  re::Status st = build_field_dfa(sub, lim, &g.pk);
   if (st == re::Status::Ok) {
     g.pats = std::move(idx);
     out->push_back(std::move(g));
@@ -96,35 +94,6 @@ int build_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> 
   if (idx.size() == 1) {
     *err = "a single pattern exceeds the DFA state/table limit";
     return L7M_ETOOBIG;
-  }
-  if (idx.size() > kChunkMinPatterns) {
-    // Large set that does not fit one group: instead of halving (a failed
-    // subset construction per level), pack patterns greedily by the explicit
-    // transitions of their own DFAs.  Patterns of one field usually diverge
-    // on a literal prefix, so a union's slots are close to the sum of its
-    // parts; a chunk that still fails falls back to halving.
-    std::vector<std::vector<uint32_t>> chunks(1);
-    uint64_t acc = 0;
-    for (uint32_t i : idx) {
-      re::Dfa one;
-      PackedDfa pk;
-      uint64_t w = kChunkSlotBudget;  // a pattern that fails alone gets a chunk of its own
-      if (re::build_dfa({asts[i]}, lim, &one) == re::Status::Ok && pack_dfa(one, &pk) == re::Status::Ok)
-        w = pk.n_explicit + 1;
-      if (!chunks.back().empty() && acc + w > kChunkSlotBudget) {
-        chunks.emplace_back();
-        acc = 0;
-      }
-      chunks.back().push_back(i);
-      acc += w;
-    }
-    if (chunks.size() > 1) {
-      for (auto& ch : chunks) {
-        int rc = build_groups(asts, std::move(ch), lim, out, err);
-        if (rc != L7M_OK) return rc;
-      }
-      return L7M_OK;
-    }
   }
   size_t h = idx.size() / 2;
   std::vector<uint32_t> a(idx.begin(), idx.begin() + h), b(idx.begin() + h, idx.end());
@@ -184,7 +153,9 @@ int translate_http_rule(const l7m_http_rule& r, std::vector<HeaderMatcher>* out,
   return L7M_OK;
 }
 
-CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts& opts) {
+namespace {
+
+CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const PolicyPlan& plan, const l7m_opts& opts) {
   CompileResult res;
   auto fail = [&](int st, const std::string& m) {
     res.status = st;
@@ -214,6 +185,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     std::string err;
     int rc = translate_http_rule(rules[i], &hm, &err);
     if (rc != L7M_OK) return fail(rc, "rule " + std::to_string(i) + ": " + err);
+    if (hm.size() > kCrMaxMatchers)
+      return fail(L7M_ETOOBIG, "rule " + std::to_string(i) + ": more than 255 header matchers");
     for (const auto& m : hm) {
       std::string lname = lower_ascii(m.name);  // Envoy LowerCaseString
       auto it = field_of.find(lname);
@@ -246,12 +219,12 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   const uint32_t nf = static_cast<uint32_t>(field_names.size());
 
   // 3. parse patterns and build DFA groups per field
-  re::DfaLimits lim;
-  // Unanchored-search DFAs of several patterns grow with the product of the
-  // patterns' progress states; fail group construction early and split.
-  if (re2) lim.max_states = 1u << 14;
-  if (opts.max_dfa_states) lim.max_states = opts.max_dfa_states;
-  if (opts.max_table_bytes) lim.max_table_bytes = opts.max_table_bytes;
+  FieldDfaLimits lim;
+  // Unanchored-search automata of several patterns grow with the product of
+  // the patterns' progress states (no pattern ever dies); split early.
+  if (re2) lim.max_multi_states = 1u << 14;
+  if (opts.max_dfa_states) lim.max_multi_states = opts.max_dfa_states;
+  if (opts.max_table_bytes) lim.max_slots = std::min<uint64_t>(lim.max_slots, opts.max_table_bytes / 4);
   std::vector<std::vector<Group>> groups(nf);
   // field pattern -> (group, local id)
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fp_loc(nf);
@@ -310,11 +283,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     for (uint32_t f = 3; f < nf; ++f) asts.push_back(re::literal_ast(field_names[f]));
     std::vector<const re::Ast*> ptrs;
     for (auto& a : asts) ptrs.push_back(&a);
-    re::DfaLimits nl;
-    nl.max_states = 1u << 22;
-    nl.max_table_bytes = 1ull << 30;
-    re::Dfa nd;
-    if (re::build_dfa(ptrs, nl, &nd) != re::Status::Ok || pack_dfa(nd, &name_dfa) != re::Status::Ok)
+    if (build_field_dfa(ptrs, FieldDfaLimits(), &name_dfa) != re::Status::Ok)
       return fail(L7M_ETOOBIG, "header-name DFA too large");
   }
 
@@ -367,8 +336,14 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   }
   for (size_t i = 0; i < n; ++i) {
     if (rule_m[i].empty()) {
-      if (!remotes[i].empty()) zero_list.push_back(static_cast<uint32_t>(i));
-      else if (always_rule == kNone) always_rule = static_cast<uint32_t>(i);
+      // matcher-less rules: the smallest unrestricted one decides outright in a
+      // one-entry map; otherwise they are checked like any other candidate
+      // (remote set, port entry)
+      if (plan.single && remotes[i].empty()) {
+        if (always_rule == kNone) always_rule = static_cast<uint32_t>(i);
+      } else {
+        zero_list.push_back(static_cast<uint32_t>(i));
+      }
       continue;
     }
     const RM* best = nullptr;
@@ -400,7 +375,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     Span s{static_cast<uint32_t>(cr.size()), static_cast<uint32_t>(rids.size())};
     for (uint32_t rid : rids) {
       cr.push_back(rid);
-      cr.push_back(static_cast<uint32_t>(rule_m[rid].size()) | (remotes[rid].empty() ? 0u : kCrRemote));
+      cr.push_back(static_cast<uint32_t>(rule_m[rid].size()) | plan.rule_entry[rid] << kCrEntryShift |
+                   (remotes[rid].empty() ? 0u : kCrRemote));
       for (const auto& m : rule_m[rid]) {
         uint32_t dfa = 0, pat = 0;
         if (m.fpat != kNone) {
@@ -487,18 +463,15 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   // ---- LDS image: descriptors always; then, hottest DFA first (header
   // names, path, authority, method, header values), slot table + u16 end
   // codes/latches; then candidate tables and set masks, within the budget.
-  uint64_t budget_bytes = opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget;
-  {
-    // The kernel's LDS also holds the per-lane end-code columns (> 8 value
-    // DFAs: 4 bytes x 1024 lanes each), the hit counters and >= 2 KiB of
-    // record stage per wave: shrink the image so many-group rule sets still
-    // launch (their tables are then walked from L2 / HBM).
-    const uint64_t codes = ndfa > kLdsRegDfas ? 4096ull * ndfa : 0;
-    const uint64_t ctr = 4ull * (n + 2);
-    const uint64_t fixed = codes + ctr + kLdsMinStageTotal;
-    budget_bytes = std::min<uint64_t>(budget_bytes, fixed < kLdsTotal ? kLdsTotal - fixed : 0);
-  }
-  const uint64_t budget = budget_bytes / 4;
+  // The kernel's LDS also holds the per-lane end-code columns (more than
+  // kHttpRegDfas value DFAs: 4 bytes x kHttpBlock lanes each), the hit
+  // counters (when they fit kMaxLdsCounters) and a record stage of at least
+  // kHttpMinStage bytes per wave (l7m_kernels.hip http_lds_bytes).  What is
+  // left bounds the table image; rule sets whose fixed part does not fit are
+  // rejected here, when the policy loads, not on every batch.
+  const uint64_t codes_bytes = ndfa > kHttpRegDfas ? 4ull * kHttpBlock * ndfa : 0;
+  const uint64_t ctr_bytes = n + 2 <= kMaxLdsCounters ? 4ull * ((n + 2 + 3) & ~uint64_t(3)) : 0;
+  const uint64_t stage_bytes = static_cast<uint64_t>(kHttpWaves) * (kHttpMinStage + 16);
   uint64_t img = 0;  // image words
   auto img_take = [&](uint64_t words) {
     uint64_t o = img;
@@ -508,6 +481,19 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   const uint32_t lds_dfas = img_take(static_cast<uint64_t>(ndt) * sizeof(DfaDesc) / 4);
   const uint32_t lds_fields = img_take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
   const uint32_t lds_name_field = img_take(name_field.size());
+  {
+    const uint64_t fixed = 4 * img + codes_bytes + ctr_bytes + stage_bytes;
+    if (fixed > kLdsBytes)
+      return fail(L7M_ETOOBIG, std::to_string(ndfa) + " value DFA groups over " + std::to_string(nf) +
+                                   " fields need " + std::to_string(fixed) + " bytes of fixed LDS (descriptors, "
+                                   "end-code columns, counters, record stage) > " + std::to_string(kLdsBytes));
+  }
+  uint64_t budget_bytes = opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget;
+  {
+    const uint64_t fixed = codes_bytes + ctr_bytes + stage_bytes;
+    budget_bytes = std::min<uint64_t>(budget_bytes, fixed < kLdsBytes ? kLdsBytes - fixed : 0);
+  }
+  const uint64_t budget = budget_bytes / 4;
   // header-name table (always resident when it fits)
   uint32_t lds_name_tab = kNone, name_slots = 0;
   std::vector<uint32_t> name_off;
@@ -516,12 +502,30 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     while (name_slots < 2 * (nf - 3)) name_slots <<= 1;
     uint64_t words = 4ull * name_slots;
     for (uint32_t f = 3; f < nf; ++f) words += ((field_names[f].size() + 3) / 4 + 3) & ~size_t(3);
-    if (4 * words <= kMaxNameTabBytes) {
+    if (4 * words <= kMaxNameTabBytes && img + words <= budget) {
       lds_name_tab = img_take(4ull * name_slots);
       for (uint32_t f = 3; f < nf; ++f) name_off.push_back(img_take((field_names[f].size() + 3) / 4));
     }
   }
-  for (uint32_t k = 0; k < ndfa; ++k) dd[k].lds_ctmask = img_take((ct[k].size() + 31) / 32);
+  // (policy, direction, port) -> port entry table (open addressing on
+  // ent_hash, program.h); in LDS when small
+  uint32_t ent_slots = 2;
+  while (ent_slots < 2 * plan.keys.size()) ent_slots <<= 1;
+  std::vector<uint32_t> ent_tab(2ull * ent_slots, 0);
+  for (const auto& kv : plan.keys) {
+    uint32_t at = ent_hash(kv.first) & (ent_slots - 1);
+    while (ent_tab[2 * at]) at = (at + 1) & (ent_slots - 1);
+    ent_tab[2 * at] = kv.first + 1;
+    ent_tab[2 * at + 1] = kv.second | (plan.entry_have_http[kv.second] ? kEntHaveHttp : 0u);
+  }
+  uint32_t lds_ent_tab = kNone;
+  if (!plan.single && 2ull * ent_slots <= kMaxLdsEntWords && img + 2ull * ent_slots <= budget)
+    lds_ent_tab = img_take(2ull * ent_slots);
+  // candidate-presence bitmasks: one bit per end code; small ones in LDS
+  for (uint32_t k = 0; k < ndfa; ++k) {
+    const uint64_t words = (ct[k].size() + 31) / 32;
+    if (words <= kMaxLdsCtmaskWords && img + words <= budget) dd[k].lds_ctmask = img_take(words);
+  }
   auto hotness = [&](uint32_t k) -> int {
     const uint32_t f = all[k].field;
     if (f == kNone) return 0;
@@ -535,13 +539,13 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hotness(a) < hotness(b); });
   for (uint32_t k : order) {
     const PackedDfa& d = *all[k].d;
-    const uint64_t half = (d.n_slots + 1) / 2;
-    const uint64_t need = ((d.n_slots + 3) & ~3ull) + 2 * ((half + 3) & ~3ull);
+    const uint64_t half_es = (d.n_slots + 1) / 2, half_latch = (d.latch.size() + 1) / 2;
+    const uint64_t need = ((d.n_slots + 3) & ~3ull) + ((half_es + 3) & ~3ull) + ((half_latch + 3) & ~3ull);
     const bool es16 = d.sets.size() < kEs16Latched && all[k].npats < kEs16Latched;
     if (es16 && img + need <= budget) {
       dd[k].lds_table = img_take(d.n_slots);
-      dd[k].lds_es = 2 * img_take(half);
-      dd[k].lds_latch = 2 * img_take(half);
+      dd[k].lds_es = 2 * img_take(half_es);
+      dd[k].lds_latch = 2 * img_take(half_latch);
     } else if (img + ((d.n_slots + 3) & ~3ull) <= budget) {
       // the slot table (read once per byte) alone; end codes / latches (read
       // once per walk) stay in the program
@@ -584,13 +588,18 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   h.off_remotes = take(static_cast<uint64_t>(n) * 2);
   h.any_remotes = any_remotes ? 1u : 0u;
   h.zero_list = zero_span;
+  h.single_entry = plan.single ? 1u : 0u;
+  h.n_policies = plan.n_policies;
+  h.ent_mask = ent_slots - 1;
+  h.ent_tab_off = take(2ull * ent_slots);
   h.off_pool = take(pool.size());
   h.off_cr = take(cr.size());
   for (uint32_t k = 0; k < ndt; ++k) {
     dd[k].table_off = take(all[k].d->n_slots);
     dd[k].es_off = take(all[k].d->n_slots);
-    dd[k].latch_off = take(all[k].d->n_slots);
+    dd[k].latch_off = take(all[k].d->latch.size());
     dd[k].ct_off = take(16 * ct[k].size());
+    dd[k].ctmask_off = take((ct[k].size() + 31) / 32);
   }
   w = (w + 63) & ~uint64_t(63);  // 256-byte aligned image
   h.lds_image_off = take(img);
@@ -599,6 +608,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   h.lds_fields = lds_fields;
   h.lds_name_field = lds_name_field;
   h.lds_name_tab = lds_name_tab;
+  h.lds_ent_tab = lds_ent_tab;
   h.name_tab_mask = lds_name_tab != kNone ? name_slots - 1 : 0;
   if (w >= (1ull << 32)) return fail(L7M_ETOOBIG, "program exceeds 16 GiB");
   h.total_words = static_cast<uint32_t>(w);
@@ -612,7 +622,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
     const PackedDfa& d = *all[k].d;
     std::memcpy(P + dd[k].table_off, d.table.data(), d.n_slots * 4ull);
     std::memcpy(P + dd[k].es_off, d.es.data(), d.n_slots * 4ull);
-    std::memcpy(P + dd[k].latch_off, d.latch.data(), d.n_slots * 4ull);
+    std::memcpy(P + dd[k].latch_off, d.latch.data(), d.latch.size() * 4ull);
     std::vector<CandEntry> ce(ct[k].size());
     std::memset(ce.data(), 0, ce.size() * sizeof(CandEntry));
     for (size_t i = 0; i < ct[k].size(); ++i) {
@@ -620,21 +630,22 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
       ce[i].len = sp.len;
       ce[i].off = sp.off;
       if (sp.len) {
-        const uint32_t nm = cr[sp.off + 1] & 0xffffu;
+        const uint32_t nm = cr_matchers(cr[sp.off + 1]);
         const uint32_t words = 2 + 2 * std::min(nm, kCandInlineMatchers);
         std::memcpy(ce[i].rec, cr.data() + sp.off, words * 4);
-        I[dd[k].lds_ctmask + i / 32] |= 1u << (i % 32);
+        P[dd[k].ctmask_off + i / 32] |= 1u << (i % 32);
+        if (dd[k].lds_ctmask != kNone) I[dd[k].lds_ctmask + i / 32] |= 1u << (i % 32);
       }
     }
     if (!ce.empty()) std::memcpy(P + dd[k].ct_off, ce.data(), ce.size() * sizeof(CandEntry));
     if (dd[k].lds_table != kNone) {
       std::memcpy(I + dd[k].lds_table, d.table.data(), d.n_slots * 4ull);
-      for (uint32_t s = 0; dd[k].lds_es != kNone && s < d.n_slots; ++s) {
+      for (uint32_t s = 0; dd[k].lds_es != kNone && s < d.n_slots; ++s)
         I16[dd[k].lds_es + s] = d.es[s] == kLatchedAccept ? static_cast<uint16_t>(kEs16Latched)
                                                            : static_cast<uint16_t>(d.es[s]);
+      for (size_t s = 0; dd[k].lds_latch != kNone && s < d.latch.size(); ++s)
         I16[dd[k].lds_latch + s] = d.latch[s] == kNone ? static_cast<uint16_t>(kEs16Latched)
                                                         : static_cast<uint16_t>(d.latch[s]);
-      }
     }
     if (dd[k].lds_ct != kNone) std::memcpy(I + dd[k].lds_ct, ce.data(), ce.size() * sizeof(CandEntry));
     if (dd[k].lds_mask != kNone) std::memcpy(I + dd[k].lds_mask, masks[k].data(), masks[k].size() * 8);
@@ -657,6 +668,8 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
       std::memcpy(I + name_off[f - 3], nm.data(), nm.size());
     }
   }
+  std::memcpy(P + h.ent_tab_off, ent_tab.data(), ent_tab.size() * 4);
+  if (lds_ent_tab != kNone) std::memcpy(I + lds_ent_tab, ent_tab.data(), ent_tab.size() * 4);
   if (!name_field.empty()) {
     std::memcpy(P + h.off_name_field, name_field.data(), name_field.size() * 4);
     std::memcpy(I + lds_name_field, name_field.data(), name_field.size() * 4);
@@ -675,6 +688,114 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   res.info.program_bytes = static_cast<uint64_t>(w) * 4;
   res.info.n_counters = static_cast<uint32_t>(n) + 2;
   return res;
+}
+
+}  // namespace
+
+CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts& opts) {
+  // one policy whose every port and direction use `rules`
+  PolicyPlan plan;
+  plan.single = true;
+  plan.n_policies = 1;
+  plan.rule_entry.assign(n, 0);
+  plan.entry_have_http = {static_cast<uint8_t>(n > 0 ? 1 : 0)};
+  plan.names = {""};
+  plan.origin.resize(n);
+  for (size_t i = 0; i < n; ++i) plan.origin[i] = {0, 1, 0, 0, static_cast<int32_t>(i), 0};
+  CompileResult r = compile_http_core(rules, n, plan, opts);
+  r.names = std::move(plan.names);
+  r.origin = std::move(plan.origin);
+  return r;
+}
+
+// NetworkPolicyMap construction (envoy/cilium_network_policy.h:40-208,
+// .cc:42-108) flattened for the kernel: every HTTP rule (or matcher-less
+// pseudo rule of a port rule without http_rules) gets an index in the order
+// l7m_rule_origin documents and the port entry it belongs to; the
+// (policy, direction, port) -> entry table drives the exact-port / port-0 /
+// no-entry selection of PortNetworkPolicy::Matches (h:169-192).
+CompileResult compile_http_policies(const l7m_network_policy* pols, size_t npol, const l7m_opts& opts) {
+  CompileResult bad;
+  auto fail = [&](int st, const std::string& m) {
+    bad.status = st;
+    bad.err = m;
+    return bad;
+  };
+  if (npol > 0 && !pols) return fail(L7M_EINVAL, "policies == NULL");
+  if (npol >= L7M_POLICY_UNKNOWN) return fail(L7M_ETOOBIG, "more than 65534 endpoint policies");
+  PolicyPlan plan;
+  plan.single = false;
+  plan.n_policies = static_cast<uint32_t>(npol);
+  std::vector<l7m_http_rule> flat;
+  std::vector<std::vector<uint32_t>> flat_remotes;  // owned copies
+  std::vector<std::string> seen_names;
+  for (size_t pi = 0; pi < npol; ++pi) {
+    const l7m_network_policy& P = pols[pi];
+    const std::string name = P.name ? P.name : "";
+    if (std::find(plan.names.begin(), plan.names.end(), name) != plan.names.end())
+      return fail(L7M_EINVAL_RULE, "duplicate endpoint policy name '" + name + "'");
+    plan.names.push_back(name);
+    for (uint32_t dir = 0; dir < 2; ++dir) {
+      const uint32_t ingress = dir == 0 ? 1u : 0u;  // ingress, then egress
+      const l7m_port_policy* pp = ingress ? P.ingress : P.egress;
+      const size_t npp = ingress ? P.n_ingress : P.n_egress;
+      if (npp && !pp) return fail(L7M_EINVAL, "port policies == NULL");
+      // port entries in input order, the port-0 entry last
+      std::vector<size_t> order;
+      std::vector<uint32_t> ports_seen;
+      for (size_t k = 0; k < npp; ++k) {
+        if (pp[k].port > 65535) return fail(L7M_EINVAL_RULE, "port > 65535");
+        if (pp[k].protocol != L7M_L4_TCP) continue;  // "NOT installing non-TCP policy" (h:163-165)
+        if (std::find(ports_seen.begin(), ports_seen.end(), pp[k].port) != ports_seen.end())
+          return fail(L7M_EINVAL_RULE, "PortNetworkPolicy: Duplicate port number " + std::to_string(pp[k].port));
+        ports_seen.push_back(pp[k].port);
+        if (pp[k].port != 0) order.push_back(k);
+      }
+      for (size_t k = 0; k < npp; ++k)
+        if (pp[k].port == 0 && pp[k].protocol == L7M_L4_TCP) order.push_back(k);
+      for (size_t k : order) {
+        const l7m_port_policy& E = pp[k];
+        if (E.n_rules && !E.rules) return fail(L7M_EINVAL, "port rules == NULL");
+        const uint32_t entry = static_cast<uint32_t>(plan.entry_have_http.size());
+        if (entry >= kCrMaxEntries) return fail(L7M_ETOOBIG, "too many port entries");
+        bool have_http = false;
+        for (size_t r = 0; r < E.n_rules; ++r) {
+          const l7m_port_rule& R = E.rules[r];
+          if (R.n_remote_ids && !R.remote_ids) return fail(L7M_EINVAL, "remote_ids == NULL");
+          std::vector<uint32_t> rem(R.remote_ids, R.remote_ids + R.n_remote_ids);
+          if (R.has_http_rules) {
+            have_http = true;
+            if (R.n_http_rules == 0 || !R.http_rules)
+              return fail(L7M_EINVAL_RULE, "http_rules present but empty (HttpNetworkPolicyRules min_items = 1)");
+            for (size_t j = 0; j < R.n_http_rules; ++j) {
+              if (R.http_rules[j].n_remote_ids)
+                return fail(L7M_EINVAL, "remote ids belong to the port rule, not to its http rules");
+              flat.push_back(R.http_rules[j]);
+              flat_remotes.push_back(rem);
+              plan.rule_entry.push_back(entry);
+              plan.origin.push_back({static_cast<uint32_t>(pi), ingress, E.port, static_cast<uint32_t>(r),
+                                     static_cast<int32_t>(j), 0});
+            }
+          } else {
+            flat.push_back(l7m_http_rule{});  // no L7 predicate: any request
+            flat_remotes.push_back(rem);
+            plan.rule_entry.push_back(entry);
+            plan.origin.push_back({static_cast<uint32_t>(pi), ingress, E.port, static_cast<uint32_t>(r), -1, 0});
+          }
+        }
+        plan.entry_have_http.push_back(have_http ? 1 : 0);
+        plan.keys.emplace_back(ent_key(static_cast<uint32_t>(pi), ingress, E.port), entry);
+      }
+    }
+  }
+  for (size_t i = 0; i < flat.size(); ++i) {
+    flat[i].remote_ids = flat_remotes[i].data();
+    flat[i].n_remote_ids = static_cast<uint32_t>(flat_remotes[i].size());
+  }
+  CompileResult r = compile_http_core(flat.data(), flat.size(), plan, opts);
+  r.names = std::move(plan.names);
+  r.origin = std::move(plan.origin);
+  return r;
 }
 
 }  // namespace l7m

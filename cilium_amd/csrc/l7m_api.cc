@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -45,6 +46,8 @@ int finish_compile(CompileResult&& cr, uint32_t proto, l7m_ruleset** out, char* 
   rs->proto = proto;
   rs->program = std::move(cr.program);
   rs->info = cr.info;
+  rs->names = std::move(cr.names);
+  rs->origin = std::move(cr.origin);
   *out = rs;
   return L7M_OK;
 }
@@ -137,6 +140,30 @@ int l7m_compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts* opt
   }
 }
 
+int l7m_compile_http_policies(const l7m_network_policy* policies, size_t n, const l7m_opts* opts,
+                              l7m_ruleset** out, char* err, size_t errlen) {
+  if (!out) return L7M_EINVAL;
+  try {
+    return finish_compile(compile_http_policies(policies, n, norm_opts(opts)), L7M_PROTO_HTTP, out, err, errlen);
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of host memory");
+    return L7M_ENOMEM;
+  }
+}
+
+int l7m_ruleset_policy_index(const l7m_ruleset* rs, const char* name) {
+  if (!rs || !name || rs->proto != L7M_PROTO_HTTP) return -1;
+  for (size_t i = 0; i < rs->names.size(); ++i)
+    if (rs->names[i] == name) return static_cast<int>(i);
+  return -1;
+}
+
+int l7m_ruleset_rule_origin(const l7m_ruleset* rs, uint32_t rule, l7m_rule_origin* out) {
+  if (!rs || !out || rs->proto != L7M_PROTO_HTTP || rule >= rs->origin.size()) return L7M_EINVAL;
+  *out = rs->origin[rule];
+  return L7M_OK;
+}
+
 void l7m_retain(l7m_ruleset* rs) {
   if (rs) rs->refs.fetch_add(1);
 }
@@ -226,7 +253,7 @@ size_t l7m_pack_http(const l7m_http_request* reqs, size_t n, uint8_t* arena, siz
     w[1] = q.remote_id;
     w[2] = q.dport | (flags << 16) | (q.n_headers << 24);
     w[3] = ml | (pl << 16);
-    w[4] = al;
+    w[4] = al | (std::min<uint32_t>(q.policy, L7M_POLICY_UNKNOWN) << 16);
     std::memcpy(r, w, sizeof w);
     size_t p = L7M_HTTP_REC_FIXED;
     for (uint32_t j = 0; j < q.n_headers; ++j) {

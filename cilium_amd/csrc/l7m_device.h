@@ -5,9 +5,29 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "program.h"
 
 namespace l7m {
+
+// Raise a kernel's dynamic-LDS limit (gfx950: up to 160 KiB per workgroup)
+// once per (kernel, device), thread-safely: l7m_eval is reentrant and a rule
+// set may be evaluated on several devices.  Returns the HIP status.
+inline hipError_t set_lds_attr_once(const void* fn, uint32_t bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count({fn, dev})) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+  if (e == hipSuccess) done.insert({fn, dev});
+  return e;
+}
 
 // LDS bytes of one HTTP workgroup with `stage` bytes of records per wave, and
 // the stage the LDS leaves after the rule tables (0: the tables do not fit).

@@ -28,10 +28,6 @@ inline uint32_t name_hash(const std::string& s) {
 
 constexpr uint32_t kDefaultLdsBudget = 48u * 1024u;  // bytes of DFA tables in the LDS image
 constexpr uint32_t kLdsCtBudget = 24u * 1024u;       // ... including candidate tables
-// HTTP kernel LDS facts the compiler sizes the image against (l7m_kernels.hip)
-constexpr uint64_t kLdsTotal = 160u * 1024u;         // gfx950 LDS per CU (one workgroup)
-constexpr uint32_t kLdsRegDfas = 8;                  // <= 8 value DFAs: end codes in registers
-constexpr uint64_t kLdsMinStageTotal = 16u * (2048u + 16u);  // 16 waves x 2 KiB stage
 
 // One getHTTPRule HeaderMatcher (pkg/envoy/server.go:261-320).
 struct HeaderMatcher {
@@ -49,6 +45,20 @@ struct CompileResult {
   std::string err;
   std::vector<uint32_t> program;
   l7m_ruleset_info info{};
+  std::vector<std::string> names;         // HTTP: endpoint policy names (index = record policy)
+  std::vector<l7m_rule_origin> origin;    // HTTP: per verdict index
+};
+
+// The port-entry structure of a compiled HTTP map (NetworkPolicyMap ->
+// PolicyInstance -> PortNetworkPolicy, envoy/cilium_network_policy.h:40-208).
+struct PolicyPlan {
+  bool single = true;                      // one entry for every policy-0 key (l7m_compile_http)
+  uint32_t n_policies = 1;
+  std::vector<uint32_t> rule_entry;        // per flattened rule
+  std::vector<std::pair<uint32_t, uint32_t>> keys;  // ent_key -> entry
+  std::vector<uint8_t> entry_have_http;    // PortNetworkPolicyRules::have_http_rules_
+  std::vector<std::string> names;
+  std::vector<l7m_rule_origin> origin;
 };
 
 int translate_http_rule(const l7m_http_rule& r, std::vector<HeaderMatcher>* out, std::string* err);
@@ -56,6 +66,7 @@ MatchKind envoy_kind(const HeaderMatcher& m);
 std::string lower_ascii(const std::string& s);
 
 CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts& opts);
+CompileResult compile_http_policies(const l7m_network_policy* pols, size_t n, const l7m_opts& opts);
 CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts& opts);
 
 }  // namespace l7m
@@ -67,6 +78,8 @@ struct l7m_ruleset {
   uint32_t proto = 0;
   std::vector<uint32_t> program;
   l7m_ruleset_info info{};
+  std::vector<std::string> names;       // HTTP endpoint policy names
+  std::vector<l7m_rule_origin> origin;  // HTTP verdict index -> NPDS position
   std::mutex mu;
   void* dprog[64] = {nullptr};  // per HIP device
 };

@@ -720,17 +720,15 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
 }
 
 template <int kHits, int kAblate = 0, bool kCliLds = false>
-static void launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
-                     uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                     unsigned long long* hits, uint32_t stage) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate, kCliLds>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kKLdsBytes);
-    attr_set = true;
-  }
+static hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
+                           uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
+                           unsigned long long* hits, uint32_t stage) {
+  const hipError_t e =
+      set_lds_attr_once(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate, kCliLds>), kKLdsBytes);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate, kCliLds>), grid, dim3(kKBlock), lds, stream, dprog, arena, arena_bytes, offs,
                      n, verdicts, hits, stage);
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -757,24 +755,20 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const uint32_t st = static_cast<uint32_t>(stage);
   if (flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) {
     if (flags & L7M_FLAG_DIAG_COPY_ONLY)
-      launch_k<kKNoHits, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
-    else
-      launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
-    return hipGetLastError();
+      return launch_k<kKNoHits, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
+    return launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
   }
 #define L7M_KAFKA_LAUNCH(M, C) \
-  launch_k<M, 0, C>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st)
+  return launch_k<M, 0, C>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st)
   if (cli_lds) {
     if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, true);
-    else if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, true);
-    else L7M_KAFKA_LAUNCH(kKGlobalHits, true);
-  } else {
-    if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, false);
-    else if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, false);
-    else L7M_KAFKA_LAUNCH(kKGlobalHits, false);
+    if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, true);
+    L7M_KAFKA_LAUNCH(kKGlobalHits, true);
   }
+  if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, false);
+  if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, false);
+  L7M_KAFKA_LAUNCH(kKGlobalHits, false);
 #undef L7M_KAFKA_LAUNCH
-  return hipGetLastError();
 }
 
 }  // namespace l7m

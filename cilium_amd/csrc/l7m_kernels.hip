@@ -25,18 +25,14 @@
 #include "l7m_device.h"
 #include "program.h"
 
-#ifndef L7M_HTTP_WAVES
-#define L7M_HTTP_WAVES 16  // waves per workgroup (one workgroup per CU)
-#endif
-
 namespace l7m {
 namespace {
 
-constexpr uint32_t kWaves = L7M_HTTP_WAVES;
-constexpr uint32_t kBlock = 64 * kWaves;
-constexpr uint32_t kMaxStage = 8192;       // bytes of records staged per wave and tile
+// geometry shared with the compiler (program.h)
+constexpr uint32_t kWaves = kHttpWaves;
+constexpr uint32_t kBlock = kHttpBlock;
+constexpr uint32_t kMaxStage = kHttpMaxStage;  // bytes of records staged per wave and tile
 constexpr uint32_t kCopyIters = kMaxStage / 1024;
-constexpr uint32_t kLdsBytes = 160 * 1024;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Where a record's bytes are read from.
@@ -72,7 +68,7 @@ __device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, c
 
 // Walk `len` bytes at byte `pos` of the record through one packed DFA
 // (dfa_pack.h): per byte ONE dependent slot-table read,
-//     e = T[base + b];  base = (e & 0xffff) == base ? e >> 16 : 0.
+//     e = T[base + b];  base = (e & 0xff) == b ? e >> 8 : 0.
 // The dead state (base 0) is absorbing, so the exit test runs once per 4
 // bytes.  kLdsTab: tables in the LDS image, else in HBM.
 template <bool kLdsTab, class Src>
@@ -84,10 +80,11 @@ __device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ img, const
   uint32_t last = kNone;
 #define L7M_STEP(B)                                        \
   {                                                        \
-    const uint32_t slot_ = base + (B);                     \
+    const uint32_t b_ = (B);                               \
+    const uint32_t slot_ = base + b_;                      \
     const uint32_t e_ = T[slot_];                          \
     last = base < region ? slot_ : last;                   \
-    base = (e_ & 0xffffu) == base ? (e_ >> 16) : 0u;       \
+    base = (e_ & 0xffu) == b_ ? (e_ >> 8) : 0u;            \
   }
   uint32_t k = 0;
   if (base) {
@@ -132,7 +129,7 @@ __device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits
 
 // Per-lane DFA end codes: in registers when the program has few value DFAs
 // (static-index select chains, no scratch), else in an LDS column.
-constexpr uint32_t kRegDfas = 8;
+constexpr uint32_t kRegDfas = kHttpRegDfas;
 template <bool kReg>
 struct Codes;
 template <>
@@ -239,6 +236,16 @@ __device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code
   return set_has(c.pool, c.sets[dd.set_base + code], p);
 }
 
+// (policy, direction, port) -> entry | kEntHaveHttp, or kNone (program.h).
+__device__ __forceinline__ uint32_t ent_lookup(const Ctx& c, const HttpHeader& h, uint32_t key) {
+  const uint32_t* tab = h.lds_ent_tab != kNone ? c.img + h.lds_ent_tab : c.prog + h.ent_tab_off;
+  for (uint32_t at = ent_hash(key) & h.ent_mask;; at = (at + 1) & h.ent_mask) {
+    const uint32_t k = tab[2 * at];
+    if (k == 0) return kNone;
+    if (k == key + 1) return tab[2 * at + 1];
+  }
+}
+
 #ifdef L7M_PROF
 // Diagnostic build only: per-lane cycle accumulators per evaluation phase
 // (s_memtime), LDS-staged records only.  prof[0] = last timestamp.
@@ -285,6 +292,37 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   if (need != w0) return L7M_VERDICT_PARSE_ERROR;
 
   if constexpr (kAblate == 2) return static_cast<int32_t>(w0 & 7u);
+
+  // Port entry selection, PortNetworkPolicy::Matches (cilium_network_policy.h
+  // :169-192) under NetworkPolicyMap::Allowed (h:223-237): the request's
+  // endpoint policy and direction select the exact-port entry `ex` and the
+  // port-0 entry `e0`; exact-port rules precede port-0 rules in the index
+  // order, so the smallest matching index is Envoy's first true.
+  uint32_t ex = 0, e0 = 0;
+  bool h0 = true;
+  {
+    const uint32_t pol = w4 >> 16;
+    if (h.single_entry) {
+      if (pol != 0) return L7M_VERDICT_DENY;  // unknown endpoint policy (h:231-235)
+      if (h.allow_no_l7) return L7M_VERDICT_ALLOW_NO_L7;
+    } else {
+      if (pol >= h.n_policies) return L7M_VERDICT_DENY;
+      const uint32_t key0 = ent_key(pol, flags & L7M_HTTP_F_INGRESS, 0);
+      const uint32_t vx = (w2 & 0xffffu) ? ent_lookup(c, h, key0 | (w2 & 0xffffu)) : kNone;
+      const uint32_t v0 = ent_lookup(c, h, key0);
+      if (vx == kNone && v0 == kNone) return L7M_VERDICT_ALLOW_NO_PORT_POLICY;
+      const uint32_t first = vx != kNone ? vx : v0;
+      if (!(first & kEntHaveHttp)) return L7M_VERDICT_ALLOW_NO_L7;  // h:129-135
+      ex = first & ~kEntHaveHttp;
+      e0 = (vx != kNone && v0 != kNone) ? (v0 & ~kEntHaveHttp) : ex;
+      h0 = (vx != kNone && v0 != kNone) ? (v0 & kEntHaveHttp) != 0 : true;
+    }
+  }
+  // a rule may decide only if it belongs to ex, or to e0 when e0 has HTTP rules
+  auto eligible = [&](uint32_t hd) -> bool {
+    const uint32_t e = cr_entry(hd);
+    return e == ex || (h0 && e == e0);
+  };
   HPROF(1);
   uint64_t present = 0;
   codes.clear(h.n_dfas);
@@ -361,9 +399,9 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
       uint32_t rw[8];
 #pragma unroll
       for (uint32_t q = 0; q < 8; ++q) rw[q] = c.cr[o + q];
-      const uint32_t rid = rw[0], nm = rw[1] & 0xffffu;
+      const uint32_t rid = rw[0], nm = cr_matchers(rw[1]);
       if (rid >= best) break;
-      bool ok = !(rw[1] & kCrRemote) || remote_ok(rid);
+      bool ok = eligible(rw[1]) && (!(rw[1] & kCrRemote) || remote_ok(rid));
       for (uint32_t q = 0; q < nm && ok; ++q) {
         const uint32_t a = q < 3 ? (q == 0 ? rw[2] : q == 1 ? rw[4] : rw[6]) : c.cr[o + 2 + 2 * q];
         const uint32_t pat = q < 3 ? (q == 0 ? rw[3] : q == 1 ? rw[5] : rw[7]) : c.cr[o + 3 + 2 * q];
@@ -382,13 +420,13 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   // record is inline; longer lists fall back to the pool scan.
   auto check_inline = [&](const uint32_t* e) {  // e -> CandEntry (LDS or HBM)
     const u32x4 q0 = reinterpret_cast<const u32x4*>(e)[0];  // len, off, rid, hdr
-    const uint32_t len = q0.x, rid = q0.z, hd = q0.w, nm = hd & 0xffffu;
+    const uint32_t len = q0.x, rid = q0.z, hd = q0.w, nm = cr_matchers(hd);
     if (len == 1 && nm <= kCandInlineMatchers) {
       if (rid >= best) return;
       const u32x4 q1 = reinterpret_cast<const u32x4*>(e)[1];
       const u32x4 q2 = reinterpret_cast<const u32x4*>(e)[2];
       const uint32_t ma[4] = {q1.x, q1.z, q2.x, q2.z}, mp[4] = {q1.y, q1.w, q2.y, q2.w};
-      bool ok = !(hd & kCrRemote) || remote_ok(rid);
+      bool ok = eligible(hd) && (!(hd & kCrRemote) || remote_ok(rid));
 #pragma unroll
       for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {
         if (q < nm && ok) {
@@ -407,7 +445,8 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     if (!code) continue;
     const DfaDesc& dd = c.dds[d];
     const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
-    if (!((c.img[dd.lds_ctmask + (idx >> 5)] >> (idx & 31u)) & 1u)) continue;  // no candidates
+    const uint32_t mw = dd.lds_ctmask != kNone ? c.img[dd.lds_ctmask + (idx >> 5)] : c.prog[dd.ctmask_off + (idx >> 5)];
+    if (!((mw >> (idx & 31u)) & 1u)) continue;  // no candidates
     if (dd.lds_ct != kNone) check_inline(c.img + dd.lds_ct + 16u * idx);
     else check_inline(c.prog + dd.ct_off + 16u * idx);
   }
@@ -419,8 +458,9 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   if (h.zero_list.len) scan(h.zero_list);
   HPROF(6);
 
-  if (h.allow_no_l7) return L7M_VERDICT_ALLOW_NO_L7;
-  return best == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(best);
+  if (best != kNone) return static_cast<int32_t>(best);
+  // the exact-port entry matched nothing; a port-0 entry without HTTP rules allows
+  return h0 ? L7M_VERDICT_DENY : L7M_VERDICT_ALLOW_NO_L7;
 }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
@@ -437,10 +477,6 @@ __device__ __forceinline__ void wave_sync() {
 // Per-rule hit counters: none, per-workgroup LDS counters flushed once at the
 // end (small rule sets), or wave-aggregated global atomics.
 enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
-#ifndef L7M_MAX_LDS_COUNTERS
-#define L7M_MAX_LDS_COUNTERS 8192
-#endif
-constexpr uint32_t kMaxLdsCounters = L7M_MAX_LDS_COUNTERS;
 
 template <int kHits, bool kReg, int kAblate>
 __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,
@@ -626,17 +662,17 @@ uint32_t http_stage_bytes(const HttpHeader& h) {
 }
 
 template <int kHits, bool kReg, int kAblate = 0>
-static void launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
+static hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, uint32_t stage) {
-  static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU)
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    attr_set = true;
-  }
+  // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU); set per device
+  // and instantiation, thread-safely (l7m_device.h)
+  const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate>),
+                                         kLdsBytes);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
                      offs, n, verdicts, hits, stage);
+  return hipGetLastError();
 }
 
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena, uint64_t arena_bytes,
@@ -655,26 +691,23 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   if (flags & (L7M_FLAG_DIAG_WALK_ONLY | L7M_FLAG_DIAG_COPY_ONLY)) {  // diagnostic ablations
     if (!reg) return hipErrorInvalidValue;
     if (flags & L7M_FLAG_DIAG_COPY_ONLY)
-      launch_one<kNoHits, true, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
-    else
-      launch_one<kNoHits, true, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
-    return hipGetLastError();
+      return launch_one<kNoHits, true, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
+    return launch_one<kNoHits, true, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
   }
   const int mode = !hits ? kNoHits : (h.n_rules + 2 <= kMaxLdsCounters ? kLdsHits : kGlobalHits);
 #define L7M_LAUNCH(M, R) \
-  launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage)
+  return launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage)
   if (mode == kNoHits) {
     if (reg) L7M_LAUNCH(kNoHits, true);
-    else L7M_LAUNCH(kNoHits, false);
-  } else if (mode == kLdsHits) {
-    if (reg) L7M_LAUNCH(kLdsHits, true);
-    else L7M_LAUNCH(kLdsHits, false);
-  } else {
-    if (reg) L7M_LAUNCH(kGlobalHits, true);
-    else L7M_LAUNCH(kGlobalHits, false);
+    L7M_LAUNCH(kNoHits, false);
   }
+  if (mode == kLdsHits) {
+    if (reg) L7M_LAUNCH(kLdsHits, true);
+    L7M_LAUNCH(kLdsHits, false);
+  }
+  if (reg) L7M_LAUNCH(kGlobalHits, true);
+  L7M_LAUNCH(kGlobalHits, false);
 #undef L7M_LAUNCH
-  return hipGetLastError();
 }
 
 }  // namespace l7m

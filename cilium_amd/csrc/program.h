@@ -19,7 +19,7 @@
 
 namespace l7m {
 
-constexpr uint32_t kMagicHttp = 0x3348374cu;   // "L7H3" (packed DFA + check records)
+constexpr uint32_t kMagicHttp = 0x3448374cu;   // "L7H4" (24-bit packed DFA + check records)
 constexpr uint32_t kMagicKafka = 0x504b374cu;  // "L7KP"
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kMaxFields = 64;            // present-mask is one u64 per request
@@ -36,8 +36,8 @@ struct Span {
 
 // One DFA group in packed double-array form (dfa_pack.h).  A walk starts at
 // start_base and performs, per input byte b,
-//     e = T[base + b];  base = (e & 0xffff) == base ? e >> 16 : 0   (0 = dead)
-// over the u32 slot table T.  The walk's end code is es[base]: 0 (no
+//     e = T[base + b];  base = (e & 0xff) == b ? e >> 8 : 0   (0 = dead)
+// over the u32 slot table T (24-bit bases, byte-label ownership check).  The walk's end code is es[base]: 0 (no
 // pattern), a set id (< nsets), or kLatchedAccept (0x80000000) meaning "the
 // latched pattern" = latch[slot of the transition that entered the latched
 // region (bases >= region)], or start_latch.  Codes are folded into one u32:
@@ -65,8 +65,9 @@ struct DfaDesc {
   uint32_t set_base;     // index of this DFA's set 0 in sets[] (pattern lists)
   uint32_t field;        // field this DFA evaluates (kNone for the name DFA)
   uint32_t nstates;
-  uint32_t lds_ctmask;   // LDS image word offset of a bitmask: ct entry i has candidates
-  uint32_t pad[5];
+  uint32_t lds_ctmask;   // LDS image word offset of a bitmask: ct entry i has candidates, or kNone
+  uint32_t ctmask_off;   // program: the same bitmask (always)
+  uint32_t pad[4];
 };
 static_assert(sizeof(DfaDesc) == 96, "dfa desc is 24 words");
 
@@ -85,16 +86,46 @@ static_assert(sizeof(CandEntry) == 64, "cand entry is 16 words");
 constexpr uint32_t kLatchedBit = 0x80000000u;
 constexpr uint32_t kEs16Latched = 0xffffu;
 
+// ---- HTTP kernel geometry and LDS budget -------------------------------
+// Shared by the compiler's LDS image sizing (http_compile.cc) and the kernel
+// (l7m_kernels.hip), so both sides agree on what the fixed part costs.
+#ifndef L7M_HTTP_WAVES
+#define L7M_HTTP_WAVES 16  // waves per workgroup (one workgroup per CU)
+#endif
+constexpr uint32_t kHttpWaves = L7M_HTTP_WAVES;
+constexpr uint32_t kHttpBlock = 64 * kHttpWaves;
+constexpr uint32_t kLdsBytes = 160u * 1024u;     // gfx950 LDS per CU (one workgroup)
+constexpr uint32_t kHttpRegDfas = 8;             // <= 8 value DFAs: end codes in registers
+constexpr uint32_t kMaxLdsCounters = 8192;       // per-rule hit counters kept in LDS up to this
+constexpr uint32_t kHttpMinStage = 2048;         // smallest record stage per wave (bytes)
+constexpr uint32_t kHttpMaxStage = 8192;         // largest record stage per wave (bytes)
+constexpr uint32_t kMaxLdsCtmaskWords = 256;     // candidate-presence bitmask kept in LDS up to this
+
 struct FieldDesc {
   uint32_t dfa_first, ndfa;  // value DFAs of this field (contiguous)
   Span presence;             // check-record list keyed on "field present"
 };
 
 // Check record (u32 words, in the check-record pool; lists are sorted by rid):
-//   [0] rule id   [1] n_matchers | (has_remote_set << 31)
+//   [0] rule id   [1] n_matchers | port entry << 8 | (has_remote_set << 31)
 //   then per matcher: [field | kind << 8 | dfa << 9] [pattern]
 // kind 0 = the DFA's end code must contain `pattern`, 1 = field present.
 constexpr uint32_t kCrRemote = 0x80000000u;
+constexpr uint32_t kCrEntryShift = 8;
+constexpr uint32_t kCrMaxMatchers = 255;
+constexpr uint32_t kCrMaxEntries = 1u << 22;
+__host__ __device__ inline uint32_t cr_matchers(uint32_t hd) { return hd & 0xffu; }
+__host__ __device__ inline uint32_t cr_entry(uint32_t hd) { return (hd >> kCrEntryShift) & (kCrMaxEntries - 1); }
+
+// Port entries: (endpoint policy, direction, port) -> entry id, the rule sets
+// of one PortNetworkPolicy (envoy/cilium_network_policy.h:152-195).  Table of
+// 2-word slots {key + 1 (0 = empty), entry | have_http << 31}.
+constexpr uint32_t kEntHaveHttp = 0x80000000u;
+constexpr uint32_t kMaxLdsEntWords = 1024;
+__host__ __device__ inline uint32_t ent_key(uint32_t policy, uint32_t ingress, uint32_t port) {
+  return policy << 17 | (ingress ? 1u : 0u) << 16 | (port & 0xffffu);
+}
+__host__ __device__ inline uint32_t ent_hash(uint32_t key) { return (key * 0x9e3779b1u) >> 7; }
 
 struct HttpHeader {
   uint32_t magic;
@@ -121,7 +152,12 @@ struct HttpHeader {
   uint32_t total_words;
   uint32_t lds_name_tab;   // LDS image offset of the header-name table, or kNone
   uint32_t name_tab_mask;  // its slot count - 1 (power of two)
-  uint32_t pad[7];         // header = 32 words
+  uint32_t single_entry;   // 1: every policy-0 request uses entry 0 (l7m_compile_http)
+  uint32_t n_policies;     // endpoint policies (record policy field < n_policies)
+  uint32_t ent_tab_off;    // program: port-entry table
+  uint32_t lds_ent_tab;    // LDS image copy, or kNone
+  uint32_t ent_mask;       // its slot count - 1
+  uint32_t pad[2];         // header = 32 words
 };
 // Header-name table (LDS image): exact lower-case header names of the rules
 // -> field id, open addressing on the program.h name hash; slot =

@@ -37,6 +37,9 @@ VERDICT_DENY = -1
 VERDICT_PARSE_ERROR = -2
 VERDICT_UNSUPPORTED = -3
 VERDICT_ALLOW_NO_L7 = 0x7FFFFFFF
+VERDICT_ALLOW_NO_PORT_POLICY = 0x7FFFFFFE
+POLICY_UNKNOWN = 0xFFFF
+L4_TCP, L4_UDP = 0, 1
 
 DIALECT_ENVOY_ECMA_FULL = 0
 DIALECT_RE2_SEARCH = 1
@@ -56,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "l7m_ruleset_get_info", "l7m_ruleset_program", "l7m_http_translate",
     "l7m_http_record_size", "l7m_pack_http", "l7m_eval", "l7m_eval_device",
     "l7m_alloc_pinned", "l7m_free_pinned", "l7m_abi_version", "l7m_device_count",
+    "l7m_compile_http_policies", "l7m_ruleset_policy_index", "l7m_ruleset_rule_origin",
 )
 
 
@@ -102,7 +106,28 @@ class _HttpReq(ctypes.Structure):
                 ("header_names", ctypes.POINTER(ctypes.c_char_p)),
                 ("header_values", ctypes.POINTER(ctypes.c_char_p)),
                 ("n_headers", ctypes.c_uint32), ("remote_id", ctypes.c_uint32),
-                ("dport", ctypes.c_uint16), ("ingress", ctypes.c_uint16)]
+                ("dport", ctypes.c_uint16), ("ingress", ctypes.c_uint16), ("policy", ctypes.c_uint32)]
+
+
+class _PortRule(ctypes.Structure):
+    _fields_ = [("remote_ids", ctypes.POINTER(ctypes.c_uint32)), ("n_remote_ids", ctypes.c_uint32),
+                ("has_http_rules", ctypes.c_uint32), ("http_rules", ctypes.POINTER(_HttpRule)),
+                ("n_http_rules", ctypes.c_size_t)]
+
+
+class _PortPolicy(ctypes.Structure):
+    _fields_ = [("port", ctypes.c_uint32), ("protocol", ctypes.c_uint32),
+                ("rules", ctypes.POINTER(_PortRule)), ("n_rules", ctypes.c_size_t)]
+
+
+class _NetworkPolicy(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("ingress", ctypes.POINTER(_PortPolicy)), ("n_ingress", ctypes.c_size_t),
+                ("egress", ctypes.POINTER(_PortPolicy)), ("n_egress", ctypes.c_size_t)]
+
+
+class _RuleOrigin(ctypes.Structure):
+    _fields_ = [("policy", ctypes.c_uint32), ("ingress", ctypes.c_uint32), ("port", ctypes.c_uint32),
+                ("port_rule", ctypes.c_uint32), ("http_rule", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
 
 
 def _load() -> ctypes.CDLL:
@@ -125,6 +150,10 @@ def _load() -> ctypes.CDLL:
                                      ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.l7m_compile_kafka.argtypes = [ctypes.POINTER(_KafkaRule), sz, ctypes.POINTER(_Opts),
                                       ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.l7m_compile_http_policies.argtypes = [ctypes.POINTER(_NetworkPolicy), sz, ctypes.POINTER(_Opts),
+                                              ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.l7m_ruleset_policy_index.argtypes = [P, ctypes.c_char_p]
+    lib.l7m_ruleset_rule_origin.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(_RuleOrigin)]
     lib.l7m_release.argtypes = [P]
     lib.l7m_release.restype = None
     lib.l7m_retain.argtypes = [P]
@@ -198,6 +227,57 @@ class PortRuleKafka:
 
 
 @dataclass
+class PortNetworkPolicyRule:
+    """NPDS PortNetworkPolicyRule (envoy/cilium/npds.proto:78-95): remote
+    identities (empty = any) and, if HttpRules is not None, their HTTP rules."""
+    RemotePolicies: Sequence[int] = field(default_factory=list)
+    HttpRules: Optional[Sequence[PortRuleHTTP]] = None
+
+
+@dataclass
+class PortNetworkPolicy:
+    """NPDS PortNetworkPolicy (npds.proto:58-76); Port 0 = any port."""
+    Port: int
+    Rules: Sequence[PortNetworkPolicyRule] = field(default_factory=list)
+    Protocol: int = 0  # L4_TCP
+
+
+@dataclass
+class NetworkPolicy:
+    """NPDS NetworkPolicy (npds.proto:32-56) of one endpoint."""
+    Name: str
+    Ingress: Sequence[PortNetworkPolicy] = field(default_factory=list)
+    Egress: Sequence[PortNetworkPolicy] = field(default_factory=list)
+
+
+def _policies_struct(policies: Sequence[NetworkPolicy], keep: list):
+    def port_policies(pps):
+        arr = (_PortPolicy * max(1, len(pps)))()
+        for k, pp in enumerate(pps):
+            rules = (_PortRule * max(1, len(pp.Rules)))()
+            for j, pr in enumerate(pp.Rules):
+                rem = (ctypes.c_uint32 * max(1, len(pr.RemotePolicies)))(*list(pr.RemotePolicies))
+                hr = list(pr.HttpRules) if pr.HttpRules is not None else []
+                harr = (_HttpRule * max(1, len(hr)))(*[_http_rule_struct(r, keep) for r in hr])
+                keep.extend([rem, harr])
+                rules[j] = _PortRule(ctypes.cast(rem, ctypes.POINTER(ctypes.c_uint32)), len(pr.RemotePolicies),
+                                     1 if pr.HttpRules is not None else 0,
+                                     ctypes.cast(harr, ctypes.POINTER(_HttpRule)), len(hr))
+            keep.append(rules)
+            arr[k] = _PortPolicy(pp.Port, pp.Protocol, ctypes.cast(rules, ctypes.POINTER(_PortRule)), len(pp.Rules))
+        keep.append(arr)
+        return ctypes.cast(arr, ctypes.POINTER(_PortPolicy)), len(pps)
+
+    out = (_NetworkPolicy * max(1, len(policies)))()
+    for i, p in enumerate(policies):
+        ing, ni = port_policies(p.Ingress)
+        eg, ne = port_policies(p.Egress)
+        out[i] = _NetworkPolicy(_b(p.Name), ing, ni, eg, ne)
+    keep.append(out)
+    return out
+
+
+@dataclass
 class HeaderMatcher:
     """envoy_api_v2_route.HeaderMatcher as emitted by getHTTPRule."""
     Name: str
@@ -219,6 +299,7 @@ class HTTPRequest:
     remote_id: int = 0
     dport: int = 80
     ingress: bool = True
+    policy: int = 0  # endpoint policy index (RuleSet.policy_index); POLICY_UNKNOWN = deny
 
 
 def _http_rule_struct(r: PortRuleHTTP, keep: list) -> _HttpRule:
@@ -263,7 +344,7 @@ def pack_http(reqs: Sequence[HTTPRequest]) -> Tuple[np.ndarray, np.ndarray]:
         arr[i] = _HttpReq(_b(q.method), _b(q.path), _b(q.authority),
                           ctypes.cast(names, ctypes.POINTER(ctypes.c_char_p)),
                           ctypes.cast(vals, ctypes.POINTER(ctypes.c_char_p)),
-                          len(q.headers), q.remote_id, q.dport, 1 if q.ingress else 0)
+                          len(q.headers), q.remote_id, q.dport, 1 if q.ingress else 0, q.policy)
         sz = _lib.l7m_http_record_size(ctypes.byref(arr[i]))
         if sz == 0:
             raise L7Error(L7M_EINVAL, f"request {i} is not encodable")
@@ -348,6 +429,33 @@ class RuleSet:
         return cls(out.value, PROTO_HTTP)
 
     @classmethod
+    def compile_http_policies(cls, policies: Sequence[NetworkPolicy], dialect: int = DIALECT_ENVOY_ECMA_FULL,
+                              lds_budget_bytes: int = 0) -> "RuleSet":
+        """A NetworkPolicyMap of NPDS NetworkPolicy resources (l7m_compile_http_policies)."""
+        keep: list = []
+        arr = _policies_struct(policies, keep)
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        opts = cls._opts(dialect, 0, 0, lds_budget_bytes)
+        rc = _lib.l7m_compile_http_policies(arr, len(policies), ctypes.byref(opts), ctypes.byref(out), err, 1024)
+        if rc != L7M_OK:
+            raise L7Error(rc, err.value.decode(errors="replace"))
+        return cls(out.value, PROTO_HTTP)
+
+    def policy_index(self, name: str) -> int:
+        """Record policy field for an endpoint policy name (POLICY_UNKNOWN if absent)."""
+        i = _lib.l7m_ruleset_policy_index(self._h, _b(name))
+        return POLICY_UNKNOWN if i < 0 else i
+
+    def rule_origin(self, rule: int) -> Tuple[int, bool, int, int, int]:
+        """(policy, ingress, port, port_rule, http_rule) of a verdict index."""
+        o = _RuleOrigin()
+        rc = _lib.l7m_ruleset_rule_origin(self._h, rule, ctypes.byref(o))
+        if rc != L7M_OK:
+            raise L7Error(rc, "rule index out of range")
+        return (o.policy, bool(o.ingress), o.port, o.port_rule, o.http_rule)
+
+    @classmethod
     def compile_kafka(cls, rules: Sequence[PortRuleKafka]) -> "RuleSet":
         arr = (_KafkaRule * max(1, len(rules)))(*[
             _KafkaRule(_b(r.Role) or None, _b(r.APIKey) or None, _b(r.APIVersion) or None,
@@ -392,18 +500,29 @@ class RuleSet:
 
 
 class NetworkPolicyMap:
-    """Batched mirror of Envoy's NetworkPolicyMap::Allowed for one port policy
-    (envoy/cilium_network_policy.h:223-237): Allowed(requests) -> bool[]."""
+    """Batched mirror of Envoy's NetworkPolicyMap (envoy/cilium_network_policy.h
+    :19-253): built from NPDS NetworkPolicy resources (or, as a shorthand, from
+    one []PortRuleHTTP applied to every port and direction);
+    Allowed(requests, policy_names) is NetworkPolicyMap::Allowed(policy_name,
+    ingress, port, remote_id, headers) for a batch (h:223-237)."""
 
-    def __init__(self, rules: Sequence[PortRuleHTTP]):
-        self.ruleset = RuleSet.compile_http(rules)
+    def __init__(self, policies):
+        policies = list(policies)
+        if policies and isinstance(policies[0], PortRuleHTTP):
+            self.ruleset = RuleSet.compile_http(policies)
+        else:
+            self.ruleset = RuleSet.compile_http_policies(policies)
 
-    def verdicts(self, reqs: Sequence[HTTPRequest]) -> np.ndarray:
+    def verdicts(self, reqs: Sequence[HTTPRequest], policy_names: Optional[Sequence[str]] = None) -> np.ndarray:
+        if policy_names is not None:
+            idx = {n: self.ruleset.policy_index(n) for n in set(policy_names)}
+            reqs = [HTTPRequest(q.method, q.path, q.authority, q.headers, q.remote_id, q.dport, q.ingress,
+                                idx[n]) for q, n in zip(reqs, policy_names)]
         arena, offs = pack_http(reqs)
         return self.ruleset.eval(arena, offs)
 
-    def Allowed(self, reqs: Sequence[HTTPRequest]) -> np.ndarray:
-        v = self.verdicts(reqs)
+    def Allowed(self, reqs: Sequence[HTTPRequest], policy_names: Optional[Sequence[str]] = None) -> np.ndarray:
+        v = self.verdicts(reqs, policy_names)
         return (v >= 0)
 
 

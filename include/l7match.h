@@ -16,6 +16,13 @@
  *   l7m_compile_kafka  replaces PortRuleKafka.Sanitize
  *                      (pkg/policy/api/rule_validation.go:190-233) applied to the
  *                      rule slice handed to MatchesRule (pkg/kafka/policy.go:200).
+ *   l7m_compile_http_policies
+ *                      the rule import of whole NPDS NetworkPolicy resources
+ *                      (envoy/cilium/npds.proto:32-118) into Envoy's
+ *                      NetworkPolicyMap (envoy/cilium_network_policy.cc:42-108,
+ *                      PolicyInstance / PortNetworkPolicy construction
+ *                      envoy/cilium_network_policy.h:40-208): per endpoint policy
+ *                      name, ingress and egress per-port rule sets.
  *   l7m_eval           replaces, for a batch of N requests,
  *                        HTTP : NetworkPolicyMap::Allowed
  *                               envoy/cilium_network_policy.h:223-237 (-> :198-203,
@@ -48,7 +55,7 @@
 extern "C" {
 #endif
 
-#define L7M_ABI_VERSION 1
+#define L7M_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define L7M_OK 0
@@ -66,6 +73,9 @@ extern "C" {
 #define L7M_VERDICT_UNSUPPORTED (-3)  /* Kafka: compressed message set (gzip/snappy) */
 #define L7M_VERDICT_ALLOW_NO_L7 (0x7fffffff) /* HTTP rule list empty: port has no L7
                                         rules, Envoy allows (cilium_network_policy.h:129-135) */
+#define L7M_VERDICT_ALLOW_NO_PORT_POLICY (0x7ffffffe) /* no per-port policy for the
+                                        request's port, not even port 0: Envoy allows
+                                        (cilium_network_policy.h:187-191) */
 
 /* ---- dialects ------------------------------------------------------------ */
 #define L7M_DIALECT_ENVOY_ECMA_FULL 0 /* std::regex ECMAScript, regex_match (full)  */
@@ -90,6 +100,61 @@ typedef struct {
   uint32_t n_remote_ids;
   const uint32_t* remote_ids;
 } l7m_http_rule;
+
+/* ---- NPDS network policies (the full NetworkPolicyMap::Allowed boundary) --
+ * PortNetworkPolicyRule (npds.proto:78-95; cilium_network_policy.h:76-112):
+ * remote identities (empty = any) and, when has_http_rules != 0, the OR of its
+ * HTTP rules (each an AND of getHTTPRule matchers; the rules' own remote_ids
+ * must be empty).  has_http_rules == 0 = no L7 predicate: any request from an
+ * allowed remote matches.  has_http_rules with n_http_rules == 0 violates
+ * HttpNetworkPolicyRules.http_rules min_items = 1 (L7M_EINVAL_RULE). */
+typedef struct {
+  const uint32_t* remote_ids;
+  uint32_t n_remote_ids;
+  uint32_t has_http_rules;
+  const l7m_http_rule* http_rules;
+  size_t n_http_rules;
+} l7m_port_rule;
+
+#define L7M_L4_TCP 0 /* envoy SocketAddress.Protocol: only TCP policies are installed */
+#define L7M_L4_UDP 1
+
+/* PortNetworkPolicy (npds.proto:58-76): port 0 = every port.  A port may
+ * appear once per direction (else L7M_EINVAL_RULE, Envoy's "Duplicate port
+ * number"); non-TCP entries are skipped as Envoy does
+ * (cilium_network_policy.h:154-166). */
+typedef struct {
+  uint32_t port;
+  uint32_t protocol; /* L7M_L4_* */
+  const l7m_port_rule* rules;
+  size_t n_rules;
+} l7m_port_policy;
+
+/* NetworkPolicy (npds.proto:32-56) of one endpoint, keyed by name. */
+typedef struct {
+  const char* name;
+  const l7m_port_policy* ingress;
+  size_t n_ingress;
+  const l7m_port_policy* egress;
+  size_t n_egress;
+} l7m_network_policy;
+
+/* Where a verdict's rule index comes from (l7m_ruleset_rule_origin).  The
+ * index space of l7m_compile_http_policies is the policies' HTTP rules
+ * flattened in this order: policies as given; ingress, then egress; port
+ * entries as given except that the port-0 entry of a direction comes last
+ * (so the smallest matching index is the exact-port match Envoy checks first,
+ * cilium_network_policy.h:169-186); port rules as given; a port rule with
+ * has_http_rules == 0 contributes one matcher-less pseudo rule
+ * (http_rule = -1), else one index per HTTP rule. */
+typedef struct {
+  uint32_t policy;    /* index into the compiled policies               */
+  uint32_t ingress;   /* 1 ingress, 0 egress                            */
+  uint32_t port;      /* PortNetworkPolicy.port (0 = wildcard)          */
+  uint32_t port_rule; /* index into that PortNetworkPolicy's rules      */
+  int32_t http_rule;  /* index into the port rule's http_rules, or -1   */
+  uint32_t reserved;
+} l7m_rule_origin;
 
 /* Verbatim api.PortRuleKafka (pkg/policy/api/kafka.go:26-106).  NULL or "" = unset. */
 typedef struct {
@@ -127,6 +192,18 @@ int l7m_compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts* opts,
                      l7m_ruleset** out, char* err, size_t errlen);
 int l7m_compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts* opts,
                       l7m_ruleset** out, char* err, size_t errlen);
+/* A NetworkPolicyMap of n endpoint policies.  A request names its policy by
+ * index in the record (l7m_ruleset_policy_index; 0xffff = a name the map does
+ * not hold -> deny, cilium_network_policy.h:231-235); its direction and dport
+ * select the per-port rule sets (exact port, then port 0, then allow).
+ * l7m_compile_http(rules, n) is the one-policy map whose every port and
+ * direction use `rules`. */
+int l7m_compile_http_policies(const l7m_network_policy* policies, size_t n, const l7m_opts* opts,
+                              l7m_ruleset** out, char* err, size_t errlen);
+/* Index of an endpoint policy name in the record's policy field, or -1. */
+int l7m_ruleset_policy_index(const l7m_ruleset* rs, const char* name);
+/* Origin of verdict index `rule` (L7M_EINVAL if out of range). */
+int l7m_ruleset_rule_origin(const l7m_ruleset* rs, uint32_t rule, l7m_rule_origin* out);
 void l7m_retain(l7m_ruleset* rs);
 void l7m_release(l7m_ruleset* rs);
 int l7m_ruleset_get_info(const l7m_ruleset* rs, l7m_ruleset_info* out);
@@ -158,7 +235,9 @@ int l7m_http_translate(const l7m_http_rule* rule, l7m_header_matcher* out, size_
  *   u16 dport          destination port
  *   u8  flags          L7M_HTTP_F_*
  *   u8  n_hdr          number of regular headers
- *   u16 method_len, u16 path_len, u16 authority_len, u16 reserved
+ *   u16 method_len, u16 path_len, u16 authority_len, u16 policy
+ *                      policy: endpoint policy index (l7m_ruleset_policy_index),
+ *                      0xffff = unknown endpoint policy (deny)
  *   n_hdr x { u16 name_len, u16 value_len }           header directory
  *   method | path | authority | name0 | value0 | name1 | value1 | ...
  * Header names must already be lower case (Envoy's codec lower-cases them);
@@ -184,7 +263,9 @@ typedef struct {
   uint32_t remote_id;
   uint16_t dport;
   uint16_t ingress;
+  uint32_t policy;  /* endpoint policy index (0 for l7m_compile_http rule sets) */
 } l7m_http_request;
+#define L7M_POLICY_UNKNOWN 0xffffu
 
 /* Bytes one request occupies in the arena (4-byte padded); 0 if not encodable. */
 size_t l7m_http_record_size(const l7m_http_request* req);

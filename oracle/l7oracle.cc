@@ -17,6 +17,10 @@
 //                          == for literal values, presence otherwise.
 //   OR over rules          envoy/cilium_network_policy.h:98-105 (first index reported)
 //   no HTTP rules -> allow envoy/cilium_network_policy.h:129-135
+//   NPDS policy maps       PolicyOracle: PortNetworkPolicyRule / PortNetworkPolicyRules /
+//                          PortNetworkPolicy / PolicyInstance / NetworkPolicyMap::Allowed
+//                          envoy/cilium_network_policy.h:76-237 (exact port, port 0,
+//                          no entry -> allow; unknown endpoint policy -> deny)
 // Kafka:
 //   Sanitize               pkg/policy/api/rule_validation.go:190-233,
 //                          MapRoleToAPIKey pkg/policy/api/kafka.go:274-293
@@ -27,11 +31,13 @@
 //                          decoder semantics serialization.go:30-196, utils.go:9-24
 //   MatchesRule            pkg/kafka/policy.go:27-225
 // Verdict encoding matches include/l7match.h (-1 deny, i >= 0 deciding rule).
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <map>
 #include <regex>
 #include <set>
+#include <unordered_map>
 #include <string>
 #include <thread>
 #include <unordered_set>
@@ -77,6 +83,8 @@ struct HttpReq {
   bool ok = false;
   std::vector<std::pair<std::string, std::string>> headers;  // pseudo first
   uint32_t remote_id = 0;
+  uint32_t dport = 0, policy = 0;
+  bool ingress = false;
 };
 
 HttpReq parse_http(const uint8_t* arena, size_t arena_bytes, uint64_t off) {
@@ -99,6 +107,9 @@ HttpReq parse_http(const uint8_t* arena, size_t arena_bytes, uint64_t off) {
   }
   if (need != len) return q;
   q.remote_id = w[1];
+  q.dport = w[2] & 0xffff;
+  q.ingress = (flags & L7M_HTTP_F_INGRESS) != 0;
+  q.policy = w[4] >> 16;
   size_t p = L7M_HTTP_REC_FIXED + 4ull * nh;
   auto take = [&](uint32_t l) {
     std::string s(reinterpret_cast<const char*>(r + p), l);
@@ -145,6 +156,131 @@ int32_t eval_http_one(const HttpOracle& o, const HttpReq& q) {
 }
 
 // ============================================================= Kafka ====
+// getHTTPRule (pkg/envoy/server.go:261-320) + SortHeaderMatchers
+// (pkg/envoy/sort.go:205-250) + Envoy HeaderData construction.
+int build_http_rule(const l7m_http_rule& r, std::vector<HeaderData>* out, std::string* err) {
+  std::vector<Matcher> ms;
+  if (!S(r.path).empty()) ms.push_back({":path", S(r.path), true});
+  if (!S(r.method).empty()) ms.push_back({":method", S(r.method), true});
+  if (!S(r.host).empty()) ms.push_back({":authority", S(r.host), true});
+  for (uint32_t j = 0; j < r.n_headers; ++j) {
+    std::string h = S(r.headers[j]);
+    size_t sp = h.find(' ');
+    if (sp != std::string::npos) {
+      std::string k = h.substr(0, sp);
+      while (!k.empty() && k.back() == ':') k.pop_back();
+      ms.push_back({k, h.substr(sp + 1), false});
+    } else {
+      ms.push_back({h, "", false});
+    }
+  }
+  for (size_t a = 0; a < ms.size(); ++a)
+    for (size_t b = a + 1; b < ms.size(); ++b)
+      if (ms[a].name == ms[b].name && ms[a].value == ms[b].value && !(ms[a].has_regex && ms[b].has_regex)) {
+        *err = "sort panic: duplicate header matcher";
+        return L7M_EINVAL_RULE;
+      }
+  std::sort(ms.begin(), ms.end(), hm_less);
+  for (auto& m : ms) {
+    if (m.name.empty()) {
+      *err = "empty header name";
+      return L7M_EINVAL_RULE;
+    }
+    HeaderData hd;
+    hd.lname = m.name;
+    for (auto& c : hd.lname) c = (char)tolower((unsigned char)c);
+    hd.value = m.value;
+    if (m.value.empty()) hd.kind = 2;
+    else if (m.has_regex) {
+      hd.kind = 0;
+      try {
+        hd.re = std::regex(m.value, std::regex::optimize);
+      } catch (const std::regex_error& e) {
+        *err = std::string("regex: ") + e.what();
+        return L7M_EINVAL_REGEX;
+      }
+    } else hd.kind = 1;
+    out->push_back(std::move(hd));
+  }
+  return L7M_OK;
+}
+
+// ConfigUtility::matchHeaders (HttpNetworkPolicyRule::Matches, h:68-71).
+bool match_headers(const std::vector<HeaderData>& hds, const HttpReq& q, bool search) {
+  for (const auto& hd : hds) {
+    const std::string* v = nullptr;
+    for (const auto& h : q.headers)
+      if (h.first == hd.lname) {
+        v = &h.second;
+        break;
+      }
+    if (!v) return false;
+    if (hd.kind == 0 && !(search ? std::regex_search(*v, hd.re) : std::regex_match(*v, hd.re))) return false;
+    if (hd.kind == 1 && *v != hd.value) return false;
+  }
+  return true;
+}
+
+struct OPortRule {  // PortNetworkPolicyRule (h:76-112)
+  std::unordered_set<uint32_t> remotes;
+  std::vector<std::vector<HeaderData>> http;
+  int32_t base = 0;  // flattened index of its first HTTP rule
+  // Matches (h:90-108): the deciding index, or -1
+  int32_t matches(uint32_t remote_id, const HttpReq& q, bool search) const {
+    if (!remotes.empty() && !remotes.count(remote_id)) return -1;
+    if (!http.empty()) {
+      for (size_t j = 0; j < http.size(); ++j)
+        if (match_headers(http[j], q, search)) return base + static_cast<int32_t>(j);
+      return -1;
+    }
+    return base;  // empty set matches any payload
+  }
+};
+struct OPortRules {  // PortNetworkPolicyRules (h:114-150)
+  std::vector<OPortRule> rules;
+  bool have_http = false;
+  int32_t matches(uint32_t remote_id, const HttpReq& q, bool search) const {
+    if (!have_http) return L7M_VERDICT_ALLOW_NO_L7;
+    if (rules.empty()) return L7M_VERDICT_ALLOW_NO_L7;
+    for (const auto& r : rules) {
+      const int32_t v = r.matches(remote_id, q, search);
+      if (v >= 0) return v;
+    }
+    return -1;
+  }
+};
+struct OPolicy {  // PolicyInstance (h:40-208)
+  std::unordered_map<uint32_t, OPortRules> ingress, egress;
+};
+struct PolicyOracle {  // NetworkPolicyMap
+  bool search = false;
+  std::map<std::string, uint32_t> names;
+  std::vector<OPolicy> pols;
+};
+
+// PortNetworkPolicy::Matches (h:169-192) under NetworkPolicyMap::Allowed
+// (h:223-237; the record carries the endpoint policy's index).
+int32_t eval_policy_one(const PolicyOracle& o, const HttpReq& q) {
+  if (!q.ok) return L7M_VERDICT_PARSE_ERROR;
+  if (q.policy >= o.pols.size()) return L7M_VERDICT_DENY;  // no policy for the endpoint
+  const auto& m = q.ingress ? o.pols[q.policy].ingress : o.pols[q.policy].egress;
+  bool found = false;
+  auto it = m.find(q.dport);
+  if (it != m.end()) {
+    const int32_t v = it->second.matches(q.remote_id, q, o.search);
+    if (v >= 0) return v;
+    found = true;
+  }
+  it = m.find(0);
+  if (it != m.end()) {
+    const int32_t v = it->second.matches(q.remote_id, q, o.search);
+    if (v >= 0) return v;
+    found = true;
+  }
+  return found ? L7M_VERDICT_DENY : L7M_VERDICT_ALLOW_NO_PORT_POLICY;
+}
+
+
 struct KRule {
   std::vector<int16_t> keys;  // apiKeyInt
   bool has_version = false;
@@ -573,62 +709,98 @@ int orc_http_new_dialect(const l7m_http_rule* rules, size_t n, uint32_t dialect,
   auto* o = new HttpOracle();
   o->search = dialect == L7M_DIALECT_RE2_SEARCH;
   for (size_t i = 0; i < n; ++i) {
-    const l7m_http_rule& r = rules[i];
-    std::vector<Matcher> ms;
-    if (!S(r.path).empty()) ms.push_back({":path", S(r.path), true});
-    if (!S(r.method).empty()) ms.push_back({":method", S(r.method), true});
-    if (!S(r.host).empty()) ms.push_back({":authority", S(r.host), true});
-    for (uint32_t j = 0; j < r.n_headers; ++j) {
-      std::string h = S(r.headers[j]);
-      size_t sp = h.find(' ');
-      if (sp != std::string::npos) {
-        std::string k = h.substr(0, sp);
-        while (!k.empty() && k.back() == ':') k.pop_back();
-        ms.push_back({k, h.substr(sp + 1), false});
-      } else {
-        ms.push_back({h, "", false});
-      }
-    }
-    for (size_t a = 0; a < ms.size(); ++a)
-      for (size_t b = a + 1; b < ms.size(); ++b)
-        if (ms[a].name == ms[b].name && ms[a].value == ms[b].value && !(ms[a].has_regex && ms[b].has_regex)) {
-          set_err(err, errlen, "sort panic: duplicate header matcher");
-          delete o;
-          return L7M_EINVAL_RULE;
-        }
-    std::sort(ms.begin(), ms.end(), hm_less);
     std::vector<HeaderData> hds;
-    for (auto& m : ms) {
-      if (m.name.empty()) {
-        set_err(err, errlen, "empty header name");
-        delete o;
-        return L7M_EINVAL_RULE;
-      }
-      HeaderData hd;
-      hd.lname = m.name;
-      for (auto& c : hd.lname) c = (char)tolower((unsigned char)c);
-      hd.value = m.value;
-      if (m.value.empty()) hd.kind = 2;
-      else if (m.has_regex) {
-        hd.kind = 0;
-        try {
-          hd.re = std::regex(m.value, std::regex::optimize);
-        } catch (const std::regex_error& e) {
-          set_err(err, errlen, std::string("regex: ") + e.what());
-          delete o;
-          return L7M_EINVAL_REGEX;
-        }
-      } else hd.kind = 1;
-      hds.push_back(std::move(hd));
+    std::string e;
+    int rc = build_http_rule(rules[i], &hds, &e);
+    if (rc) {
+      set_err(err, errlen, e);
+      delete o;
+      return rc;
     }
     o->rules.push_back(std::move(hds));
     std::unordered_set<uint32_t> rem;
-    for (uint32_t j = 0; j < r.n_remote_ids; ++j) rem.insert(r.remote_ids[j]);
+    for (uint32_t j = 0; j < rules[i].n_remote_ids; ++j) rem.insert(rules[i].remote_ids[j]);
     o->remotes.push_back(std::move(rem));
   }
   *out = o;
   return L7M_OK;
 }
+
+// NetworkPolicyMap restated (envoy/cilium_network_policy.h:40-237,
+// npds.proto:32-118).  Verdict index = the flattened position of the deciding
+// HTTP rule in the order include/l7match.h (l7m_rule_origin) documents.
+int orc_http_policies_new(const l7m_network_policy* pols, size_t n, uint32_t dialect, void** out, char* err,
+                          size_t errlen) {
+  auto* o = new PolicyOracle();
+  o->search = dialect == L7M_DIALECT_RE2_SEARCH;
+  int32_t index = 0;
+  for (size_t pi = 0; pi < n; ++pi) {
+    const l7m_network_policy& P = pols[pi];
+    OPolicy op;
+    for (int dir = 0; dir < 2; ++dir) {
+      const l7m_port_policy* pp = dir == 0 ? P.ingress : P.egress;
+      const size_t npp = dir == 0 ? P.n_ingress : P.n_egress;
+      auto& m = dir == 0 ? op.ingress : op.egress;
+      // index order: port entries as given, the port-0 entry last
+      std::vector<size_t> order;
+      for (size_t k = 0; k < npp; ++k)
+        if (pp[k].port != 0) order.push_back(k);
+      for (size_t k = 0; k < npp; ++k)
+        if (pp[k].port == 0) order.push_back(k);
+      for (size_t k : order) {
+        if (pp[k].protocol != L7M_L4_TCP) continue;  // h:156-166
+        OPortRules prs;
+        for (size_t r = 0; r < pp[k].n_rules; ++r) {
+          const l7m_port_rule& R = pp[k].rules[r];
+          OPortRule pr;
+          for (uint32_t j = 0; j < R.n_remote_ids; ++j) pr.remotes.insert(R.remote_ids[j]);
+          pr.base = index;
+          if (R.has_http_rules) {
+            prs.have_http = true;
+            if (R.n_http_rules == 0) {
+              set_err(err, errlen, "empty http_rules");
+              delete o;
+              return L7M_EINVAL_RULE;
+            }
+            for (size_t j = 0; j < R.n_http_rules; ++j) {
+              std::vector<HeaderData> hds;
+              std::string e;
+              int rc = build_http_rule(R.http_rules[j], &hds, &e);
+              if (rc) {
+                set_err(err, errlen, e);
+                delete o;
+                return rc;
+              }
+              pr.http.push_back(std::move(hds));
+              ++index;
+            }
+          } else {
+            ++index;
+          }
+          prs.rules.push_back(std::move(pr));
+        }
+        if (!m.emplace(pp[k].port, std::move(prs)).second) {
+          set_err(err, errlen, "PortNetworkPolicy: Duplicate port number");
+          delete o;
+          return L7M_EINVAL_RULE;
+        }
+      }
+    }
+    o->names.emplace(S(P.name), static_cast<uint32_t>(pi));
+    o->pols.push_back(std::move(op));
+  }
+  *out = o;
+  return L7M_OK;
+}
+
+int orc_http_policies_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint64_t* offs, size_t n,
+                           int32_t* verdicts, int threads) {
+  const PolicyOracle& o = *static_cast<PolicyOracle*>(h);
+  parallel_for(n, threads, [&](size_t i) { verdicts[i] = eval_policy_one(o, parse_http(arena, arena_bytes, offs[i])); });
+  return L7M_OK;
+}
+
+void orc_http_policies_free(void* h) { delete static_cast<PolicyOracle*>(h); }
 
 int orc_http_new(const l7m_http_rule* rules, size_t n, void** out, char* err, size_t errlen) {
   return orc_http_new_dialect(rules, n, L7M_DIALECT_ENVOY_ECMA_FULL, out, err, errlen);

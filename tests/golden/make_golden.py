@@ -146,8 +146,34 @@ KAFKA_SANITIZE = [
 ]
 
 
+# The same BASIC_POLICY as the NPDS resource it is (name '173', ingress and
+# egress port 80, two PortNetworkPolicyRules), with the directions of the
+# ingress (:605-639, remote identity 1) and egress (:683-717, destination
+# resolved to identity 1 by the host map :670-678) tests, and the
+# DuplicatePort test (:641-659): the policy is rejected, so the endpoint has
+# no policy and every request is denied (403).
+_BASIC_PORT = {"Port": 80, "Rules": [
+    {"RemotePolicies": [1], "HttpRules": [r for r in BASIC_POLICY_RULES if r["RemoteIDs"] == [1]]},
+    {"RemotePolicies": [2], "HttpRules": [r for r in BASIC_POLICY_RULES if r["RemoteIDs"] == [2]]},
+]}
+for _r in _BASIC_PORT["Rules"]:
+    _r["HttpRules"] = [{k: v for k, v in h.items() if k != "RemoteIDs"} for h in _r["HttpRules"]]
+NPDS_BASIC = {"Name": "173", "Ingress": [_BASIC_PORT], "Egress": [_BASIC_PORT]}
+NPDS_DUPLICATE_PORT = {"Name": "173", "Ingress": [_BASIC_PORT, {"Port": 80, "Rules": [
+    {"RemotePolicies": [2], "HttpRules": [{"Headers": [":path /only-2-allowed"]}]}]}], "Egress": [_BASIC_PORT]}
+
+
 def main():
     out = {
+        "npds_basic_policy": {"source": "envoy/cilium_integration_test.cc:40-75,89-100,605-717",
+                              "policy": NPDS_BASIC, "remote_id": 1, "dport": 80,
+                              "ingress_cases": [{"name": n, "method": m, "path": p, "authority": a, "allow": ok}
+                                                for n, m, p, a, ok in BASIC_CASES],
+                              "egress_cases": [{"name": n, "method": m, "path": p, "authority": a, "allow": ok}
+                                               for n, m, p, a, ok in BASIC_CASES],
+                              "duplicate_port_policy": NPDS_DUPLICATE_PORT,
+                              "duplicate_port_case": {"name": "DuplicatePort", "method": "GET", "path": "/allowed",
+                                                      "authority": "host", "allow": False}},
         "basic_policy": {"source": "envoy/cilium_integration_test.cc:40-75,605-639,683-717",
                          "rules": BASIC_POLICY_RULES, "remote_id": 1, "dport": 80,
                          "cases": [{"name": n, "method": m, "path": p, "authority": a, "allow": ok}

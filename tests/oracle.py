@@ -23,6 +23,10 @@ def _load():
                                          ctypes.c_char_p, sz]
     lib.orc_http_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_http_free.argtypes = [P]
+    lib.orc_http_policies_new.argtypes = [ctypes.POINTER(L._NetworkPolicy), sz, ctypes.c_uint32,
+                                          ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.orc_http_policies_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
+    lib.orc_http_policies_free.argtypes = [P]
     lib.orc_kafka_new.argtypes = [ctypes.POINTER(L._KafkaRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.orc_kafka_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_kafka_free.argtypes = [P]
@@ -61,6 +65,32 @@ class HttpOracle:
         v = np.empty(offsets.shape[0], dtype=np.int32)
         _lib.orc_http_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
                            offsets.shape[0], v.ctypes.data, threads)
+        return v
+
+
+class PolicyOracle:
+    """NetworkPolicyMap restated (oracle/l7oracle.cc PolicyOracle)."""
+
+    def __init__(self, policies, dialect=L.DIALECT_ENVOY_ECMA_FULL):
+        keep = []
+        arr = L._policies_struct(policies, keep)
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.orc_http_policies_new(arr, len(policies), dialect, ctypes.byref(h), err, 512)
+        if rc != 0:
+            raise OracleError(rc, err.value.decode(errors="replace"))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.orc_http_policies_free(self._h)
+
+    def eval(self, arena, offsets, threads=1):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        v = np.empty(offsets.shape[0], dtype=np.int32)
+        _lib.orc_http_policies_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
+                                    offsets.shape[0], v.ctypes.data, threads)
         return v
 
 

@@ -20,9 +20,9 @@ CR_REMOTE = 0x80000000
 HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_dfa off_dfas off_fields "
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
-              "name_tab_mask").split()
+              "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
-              "start_latch n_slots nsets npats set_base field nstates lds_ctmask").split()
+              "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off").split()
 
 
 def name_hash(data: bytes) -> int:
@@ -46,7 +46,8 @@ class HttpProgram:
         self.w = prog.astype(np.uint64).astype(np.int64).tolist()
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
         h = self.h
-        assert h["magic"] == 0x3348374C
+        assert h["magic"] == 0x3448374C
+        assert len(HDR_FIELDS) == 30
         io = h["lds_image_off"]
         self.img = self.w[io:io + h["lds_image_words"]]
         self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
@@ -90,7 +91,7 @@ class HttpProgram:
             e = T[Toff + slot]
             if base < d["region"]:
                 last = slot
-            base = e >> 16 if (e & 0xFFFF) == base else 0
+            base = e >> 8 if (e & 0xFF) == b else 0
         if not base:
             return 0
         if lds and d["lds_es"] != KNONE:  # table-only LDS placement keeps end codes in the program
@@ -120,7 +121,9 @@ class HttpProgram:
         """Candidate list (pool offset, record count) of end-code index idx;
         checks the LDS presence bit and the inlined first record."""
         d = self.dfas[k]
-        bit = (self.img[d["lds_ctmask"] + (idx >> 5)] >> (idx & 31)) & 1
+        bit = (self.w[d["ctmask_off"] + (idx >> 5)] >> (idx & 31)) & 1
+        if d["lds_ctmask"] != KNONE:
+            assert bit == (self.img[d["lds_ctmask"] + (idx >> 5)] >> (idx & 31)) & 1
         if d["lds_ct"] != KNONE:
             e = self.img[d["lds_ct"] + 16 * idx: d["lds_ct"] + 16 * idx + 16]
         else:
@@ -129,10 +132,24 @@ class HttpProgram:
         assert bit == (1 if n else 0)
         if n:
             cr = self.h["off_cr"] + off
-            nm = self.w[cr + 1] & 0xFFFF
+            nm = self.w[cr + 1] & 0xFF
             k_in = 2 + 2 * min(nm, 4)
             assert e[2:2 + k_in] == self.w[cr:cr + k_in]
         return off, n
+
+    def ent_lookup(self, key):
+        h = self.h
+        if h["lds_ent_tab"] != KNONE:
+            tab = self.img[h["lds_ent_tab"]: h["lds_ent_tab"] + 2 * (h["ent_mask"] + 1)]
+            assert tab == self.w[h["ent_tab_off"]: h["ent_tab_off"] + 2 * (h["ent_mask"] + 1)]
+        at = (((key * 0x9E3779B1) & 0xFFFFFFFF) >> 7) & h["ent_mask"]
+        while True:
+            k = self.w[h["ent_tab_off"] + 2 * at]
+            if k == 0:
+                return KNONE
+            if k == key + 1:
+                return self.w[h["ent_tab_off"] + 2 * at + 1]
+            at = (at + 1) & h["ent_mask"]
 
     def eval_record(self, rec: bytes) -> int:
         h = self.h
@@ -143,6 +160,34 @@ class HttpProgram:
         dirs = [struct.unpack_from("<I", rec, 20 + 4 * j)[0] for j in range(nhdr)]
         if 20 + 4 * nhdr + mlen + plen + alen + sum((e & 0xFFFF) + (e >> 16) for e in dirs) != w0:
             return L.VERDICT_PARSE_ERROR
+        # port entry selection (kernel: l7m_kernels.hip eval_record)
+        pol, dport = w4 >> 16, w2 & 0xFFFF
+        ex = e0 = 0
+        h0 = True
+        if h["single_entry"]:
+            if pol != 0:
+                return L.VERDICT_DENY
+            if h["allow_no_l7"]:
+                return L.VERDICT_ALLOW_NO_L7
+        else:
+            if pol >= h["n_policies"]:
+                return L.VERDICT_DENY
+            key0 = pol << 17 | (1 if flags & L.F_INGRESS else 0) << 16
+            vx = self.ent_lookup(key0 | dport) if dport else KNONE
+            v0 = self.ent_lookup(key0)
+            if vx == KNONE and v0 == KNONE:
+                return L.VERDICT_ALLOW_NO_PORT_POLICY
+            first = vx if vx != KNONE else v0
+            if not first & 0x80000000:
+                return L.VERDICT_ALLOW_NO_L7
+            ex = first & 0x7FFFFFFF
+            both = vx != KNONE and v0 != KNONE
+            e0 = (v0 & 0x7FFFFFFF) if both else ex
+            h0 = bool(v0 & 0x80000000) if both else True
+
+        def eligible(hd):
+            e = (hd >> 8) & ((1 << 22) - 1)
+            return e == ex or (h0 and e == e0)
         codes = [0] * h["n_dfas"]
         present = 0
         pos = 20 + 4 * nhdr
@@ -182,10 +227,10 @@ class HttpProgram:
             o, n = span
             for _ in range(n):
                 rid, hd = self.w[cr + o], self.w[cr + o + 1]
-                nm = hd & 0xFFFF
+                nm = hd & 0xFF
                 if rid >= best:
                     break
-                ok = not (hd & CR_REMOTE) or remote_ok(rid)
+                ok = eligible(hd) and (not (hd & CR_REMOTE) or remote_ok(rid))
                 for q in range(nm):
                     if not ok:
                         break
@@ -209,9 +254,9 @@ class HttpProgram:
             if (present >> f) & 1:
                 best = scan((self.fields[f][2], self.fields[f][3]), best)
         best = scan((h["zero_off"], h["zero_len"]), best)
-        if h["allow_no_l7"]:
-            return L.VERDICT_ALLOW_NO_L7
-        return L.VERDICT_DENY if best == KNONE else best
+        if best != KNONE:
+            return best
+        return L.VERDICT_DENY if h0 else L.VERDICT_ALLOW_NO_L7
 
     def eval(self, arena: np.ndarray, offsets: np.ndarray) -> np.ndarray:
         buf = arena.tobytes()

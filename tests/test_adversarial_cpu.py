@@ -4,6 +4,7 @@
 oracle.  Oracle limits: std::regex backtracks, so generated subjects keep
 (a|aa)* runs <= 20 characters; the long values are literal-compared."""
 import numpy as np
+import pytest
 
 from cilium_amd import workloads as W
 from cilium_amd import l7match as L
@@ -24,14 +25,31 @@ def test_adversarial_compiler_vs_oracle():
     assert (exp >= 0).any() and (exp == -1).any()
 
 
-def test_adversarial_chunked_grouping_vs_oracle():
-    """> 64 path patterns that do not fit one DFA group: estimate-based
-    chunking (http_compile.cc build_groups) then halving; verdicts unchanged."""
-    rules = W.rules(5, n_rules=160)
-    arena, offs = W.requests(5, 0, 50, n_rules=160)
+def test_adversarial_scale_one_automaton_per_field():
+    """2k adversarial rules compile into ONE packed automaton per field
+    (literal-prefix product + shared residual tails, dfa_pack.h) in seconds,
+    and the packed program agrees with the oracle."""
+    import time
+    rules = W.rules(5, n_rules=2000)
+    t = time.time()
     rs = L.RuleSet.compile_http(rules)
-    assert rs.info.n_dfas > 10
+    assert time.time() - t < 60
+    # method, path, x-blob value + the header-name automaton
+    assert rs.info.n_dfas == 4
+    arena, offs = W.requests(5, 0, 120, n_rules=2000)
     got = HttpProgram(rs.program()).eval(arena, offs)
     exp = HttpOracle(rules).eval(arena, offs, threads=8)
     bad = np.nonzero(got != exp)[0]
     assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+    assert (exp >= 0).any() and (exp == -1).any()
+
+
+def test_many_dfa_groups_are_rejected_at_compile_time():
+    """A rule set whose fixed LDS part (per-lane end-code columns of every
+    value DFA group) cannot fit the kernel is refused by l7m_compile_http,
+    where Envoy would NACK the policy, not on every batch."""
+    rules = [L.PortRuleHTTP(Path=f".*x{i}y.*") for i in range(400)]
+    with pytest.raises(L.L7Error) as e:
+        L.RuleSet.compile_http(rules, dialect=L.DIALECT_RE2_SEARCH)
+    assert e.value.code == L.L7M_ETOOBIG
+    assert "fixed LDS" in str(e.value)
