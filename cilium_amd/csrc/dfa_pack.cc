@@ -380,14 +380,17 @@ re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const Fi
   std::unordered_map<std::vector<uint64_t>, uint32_t, VecHash> set_ids;
   set_ids.emplace(std::vector<uint64_t>{}, 0);
 
-  // tails (latched nodes): literal chain nodes per (pattern, position) and
-  // the states of each used residual
-  std::unordered_map<uint64_t, uint32_t> chain_id;
-  std::vector<uint64_t> chain_items;  // tail id -> item, for chain nodes
+  // tails (latched nodes): the states of each used residual, and literal
+  // chain nodes hash-consed on (byte, next node) so that equal literal
+  // suffixes before equal residuals are one chain (config 2: the 500
+  // `/svc{i}/` rules share the "v" node in front of their common residual)
+  constexpr uint32_t kDeadTail = 0xffffffffu;
+  std::unordered_map<uint64_t, uint32_t> chain_id;  // byte << 32 | next -> tail id
+  std::vector<uint64_t> chain_key;                   // chain index -> byte << 32 | next
   std::vector<uint32_t> rbase(nres, kNoPat);
   uint32_t ntail = 0;
   std::vector<uint8_t> tail_kind;  // 0 chain, 1 residual state (for rows)
-  std::vector<uint32_t> tail_ref;  // chain: index into chain_items; residual: rid
+  std::vector<uint32_t> tail_ref;  // chain: index into chain_key; residual: rid
   auto ensure_res = [&](uint32_t r) {
     if (rbase[r] != kNoPat) return;
     rbase[r] = ntail;
@@ -400,23 +403,21 @@ re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const Fi
     const uint32_t p = static_cast<uint32_t>(item >> 32), pos = static_cast<uint32_t>(item);
     const uint32_t L = static_cast<uint32_t>(lit[p].size());
     ensure_res(rid[p]);
+    const Residual& R = res[rid[p]];
     if (pos >= L) return rbase[rid[p]] + (pos - L) - 1;
-    uint32_t first = kNoPat;
-    for (uint32_t i = pos; i < L; ++i) {
-      const uint64_t key = static_cast<uint64_t>(p) << 32 | i;
+    uint32_t next = R.start ? rbase[rid[p]] + R.start - 1 : kDeadTail;
+    for (uint32_t i = L; i-- > pos;) {
+      const uint64_t key = static_cast<uint64_t>(static_cast<uint8_t>(lit[p][i])) << 32 | next;
       auto it = chain_id.find(key);
-      if (it != chain_id.end()) {
-        if (first == kNoPat) first = it->second;
-        break;  // the rest of the chain exists
+      if (it == chain_id.end()) {
+        it = chain_id.emplace(key, ntail++).first;
+        tail_kind.push_back(0);
+        tail_ref.push_back(static_cast<uint32_t>(chain_key.size()));
+        chain_key.push_back(key);
       }
-      const uint32_t id = ntail++;
-      chain_id.emplace(key, id);
-      tail_kind.push_back(0);
-      tail_ref.push_back(static_cast<uint32_t>(chain_items.size()));
-      chain_items.push_back(key);
-      if (first == kNoPat) first = id;
+      next = it->second;
     }
-    return first;
+    return next;
   };
   std::vector<uint64_t> start_items;
   for (uint32_t p = 0; p < np; ++p) {
@@ -532,18 +533,9 @@ re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const Fi
     } else {
       const uint32_t t = row - 1 - nmulti;
       if (tail_kind[t] == 0) {
-        const uint64_t item = chain_items[tail_ref[t]];
-        const uint32_t p = static_cast<uint32_t>(item >> 32), i = static_cast<uint32_t>(item);
-        const uint32_t L = static_cast<uint32_t>(lit[p].size());
-        uint32_t tgt;
-        if (i + 1 < L) {
-          tgt = 1 + nmulti + chain_id.at(static_cast<uint64_t>(p) << 32 | (i + 1));
-        } else {
-          const Residual& R = res[rid[p]];
-          if (!R.start) return;
-          tgt = 1 + nmulti + rbase[rid[p]] + R.start - 1;
-        }
-        rb.push_back({static_cast<uint8_t>(lit[p][i]), tgt, kNoPat});
+        const uint64_t key = chain_key[tail_ref[t]];
+        const uint32_t next = static_cast<uint32_t>(key);
+        if (next != kDeadTail) rb.push_back({static_cast<uint8_t>(key >> 32), 1 + nmulti + next, kNoPat});
       } else {
         const uint32_t r = tail_ref[t];
         const Residual& R = res[r];

@@ -7,6 +7,8 @@
 
 #include <cstdio>
 #include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -79,6 +81,109 @@ int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
   return L7M_OK;
 }
 
+// ---- Kafka compressed-message second pass: per-device scratch ------------
+// The first pass queues gzip / snappy values; kafka_codec_kernel decodes them
+// in per-worker slabs.  Queues come from a small ring per device (a launch
+// waits, on its stream, for the previous user of its queue); the slabs are
+// one pool per device, so second passes of concurrent launches are chained
+// through an event.  Without the scratch (allocation failure) the queue
+// capacity is 0 and compressed values report L7M_VERDICT_UNSUPPORTED.
+constexpr int kCodecSlots = 8;
+constexpr uint32_t kCodecQueueCap = 1u << 20;
+
+struct KafkaCodecDev {
+  std::mutex mu;
+  bool init = false;
+  uint8_t* slabs = nullptr;
+  uint32_t workers = 0;
+  uint64_t slab_bytes = 0;
+  hipEvent_t p2_done = nullptr;
+  struct Slot {
+    KafkaCodecItem* items = nullptr;
+    uint32_t* qhdr = nullptr;
+    uint32_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool busy = false;  // claimed by a launch that has not recorded `done` yet
+  } slots[kCodecSlots];
+  uint32_t rr = 0;
+  std::condition_variable cv;
+};
+KafkaCodecDev g_kcodec[64];
+
+uint32_t codec_workers() {
+  const char* e = std::getenv("L7M_KAFKA_CODEC_WORKERS");
+  const long v = e ? std::strtol(e, nullptr, 10) : 64;
+  return v < 0 ? 0u : v > 4096 ? 4096u : static_cast<uint32_t>(v);
+}
+
+hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
+                             const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
+                             hipStream_t stream, int cus, uint32_t flags) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  KafkaCodecDev& g = g_kcodec[dev];
+  KafkaCodecQueue cq;
+  KafkaCodecDev::Slot* slot = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(g.mu);
+    if (!g.init) {
+      g.init = true;
+      g.workers = codec_workers();
+      // two decoded sets of maxParseBufSize always fit: nesting one level deep
+      // never runs out of slab
+      g.slab_bytes = (2ull * kKafkaMaxParseBuf + 65536 + 255) & ~255ull;
+      if (g.workers && (hipMalloc(reinterpret_cast<void**>(&g.slabs), g.workers * g.slab_bytes) != hipSuccess ||
+                        hipEventCreateWithFlags(&g.p2_done, hipEventDisableTiming) != hipSuccess)) {
+        g.slabs = nullptr;
+        g.workers = 0;
+      }
+    }
+    for (;;) {  // a free queue: its previous user has enqueued its `done` record
+      for (int k = 0; k < kCodecSlots && !slot; ++k) {
+        KafkaCodecDev::Slot* c = &g.slots[g.rr++ % kCodecSlots];
+        if (!c->busy) slot = c;
+      }
+      if (slot) break;
+      g.cv.wait(lk);
+    }
+    slot->busy = true;
+    if (!slot->qhdr) {
+      if (hipMalloc(reinterpret_cast<void**>(&slot->qhdr), 16) != hipSuccess ||
+          hipEventCreateWithFlags(&slot->done, hipEventDisableTiming) != hipSuccess) {
+        slot->busy = false;
+        return hipErrorOutOfMemory;
+      }
+      if (g.workers &&
+          hipMalloc(reinterpret_cast<void**>(&slot->items), kCodecQueueCap * sizeof(KafkaCodecItem)) == hipSuccess)
+        slot->cap = kCodecQueueCap;
+    }
+    hipError_t e = hipStreamWaitEvent(stream, slot->done, 0);
+    if (e == hipSuccess) e = hipMemsetAsync(slot->qhdr, 0, 16, stream);
+    if (e != hipSuccess) {
+      slot->busy = false;
+      return e;
+    }
+    cq.items = slot->items;
+    cq.qhdr = slot->qhdr;
+    cq.cap = g.workers ? slot->cap : 0;
+    cq.workers = g.workers;
+    cq.slabs = g.slabs;
+    cq.slab_bytes = g.slab_bytes;
+  }
+  hipError_t e = launch_kafka(dprog, h, arena, arena_bytes, offs, n, verdicts, hits, stream, cus, flags, cq);
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (e == hipSuccess && n && !(flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) && cq.cap) {
+    e = hipStreamWaitEvent(stream, g.p2_done, 0);
+    if (e == hipSuccess) e = launch_kafka_codec(dprog, arena, verdicts, hits, stream, cq);
+    if (e == hipSuccess) e = hipEventRecord(g.p2_done, stream);
+  }
+  const hipError_t e2 = hipEventRecord(slot->done, stream);
+  if (e == hipSuccess) e = e2;
+  slot->busy = false;
+  g.cv.notify_one();
+  return e;
+}
+
 int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const void* offs, size_t n, void* verdicts,
            void* hits, hipStream_t stream, uint32_t flags) {
   auto* rs = const_cast<l7m_ruleset*>(crs);
@@ -97,13 +202,77 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
   } else if (rs->proto == L7M_PROTO_KAFKA) {
     KafkaHeader h;
     std::memcpy(&h, rs->program.data(), sizeof h);
-    e = launch_kafka(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
-                     n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
-                     stream, cus, flags);
+    e = launch_kafka_both(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes,
+                          static_cast<const uint64_t*>(offs), n, static_cast<int32_t*>(verdicts),
+                          static_cast<unsigned long long*>(hits), stream, cus, flags);
   } else {
     return L7M_EINVAL;
   }
   return e == hipSuccess ? L7M_OK : L7M_EDEVICE;
+}
+
+
+// ---- l7m_eval contexts ------------------------------------------------------
+// l7m_eval is reentrant: each concurrent call takes its own context (stream +
+// device buffers grown to the largest batch seen) from a per-device free
+// list, so steady-state calls allocate nothing and never share buffers.
+constexpr int kMaxDevices = 64;
+
+struct EvalCtx {
+  hipStream_t stream = nullptr;
+  void *arena = nullptr, *offs = nullptr, *verd = nullptr, *hits = nullptr;
+  size_t cap_arena = 0, cap_offs = 0, cap_verd = 0, cap_hits = 0;
+  std::vector<uint64_t> hhost;
+  static int grow(void** p, size_t* cap, size_t want) {
+    if (*cap >= want) return L7M_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t sz = want + want / 4;  // some headroom for the next batch
+    if (hipMalloc(p, sz) != hipSuccess) {
+      *p = nullptr;
+      return L7M_ENOMEM;
+    }
+    *cap = sz;
+    return L7M_OK;
+  }
+  int reserve(size_t abytes, size_t n, size_t nctr) {
+    int rc = grow(&arena, &cap_arena, abytes);
+    if (rc == L7M_OK) rc = grow(&offs, &cap_offs, n * 8);
+    if (rc == L7M_OK) rc = grow(&verd, &cap_verd, n * 4);
+    if (rc == L7M_OK) rc = grow(&hits, &cap_hits, nctr * 8);
+    if (rc == L7M_OK) hhost.resize(nctr);
+    return rc;
+  }
+};
+
+struct CtxPool {
+  std::mutex mu;
+  std::vector<EvalCtx*> free;
+};
+CtxPool g_pools[kMaxDevices];
+
+EvalCtx* acquire_ctx(int dev) {
+  {
+    std::lock_guard<std::mutex> g(g_pools[dev].mu);
+    if (!g_pools[dev].free.empty()) {
+      EvalCtx* c = g_pools[dev].free.back();
+      g_pools[dev].free.pop_back();
+      return c;
+    }
+  }
+  auto* c = new (std::nothrow) EvalCtx();
+  if (!c) return nullptr;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void release_ctx(int dev, EvalCtx* c) {
+  std::lock_guard<std::mutex> g(g_pools[dev].mu);
+  g_pools[dev].free.push_back(c);
 }
 
 }  // namespace
@@ -299,43 +468,31 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return L7M_EDEVICE;
   if (n == 0) return L7M_OK;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return L7M_EDEVICE;
   const size_t nctr = rs->info.n_counters;
-  hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return L7M_EDEVICE;
-  void *da = nullptr, *doff = nullptr, *dv = nullptr, *dh = nullptr;
-  int rc = L7M_OK;
-  auto cleanup = [&]() {
-    if (da) (void)hipFree(da);
-    if (doff) (void)hipFree(doff);
-    if (dv) (void)hipFree(dv);
-    if (dh) (void)hipFree(dh);
-    (void)hipStreamDestroy(st);
-  };
   // Pad the arena copy so that the kernels' aligned word loads never run past it.
-  size_t abytes = (arena_bytes + 64) & ~size_t(3);
-  if (hipMalloc(&da, abytes) != hipSuccess || hipMalloc(&doff, n * 8) != hipSuccess ||
-      hipMalloc(&dv, n * 4) != hipSuccess || (hits && hipMalloc(&dh, nctr * 8) != hipSuccess)) {
-    cleanup();
-    return L7M_ENOMEM;
+  const size_t abytes = (arena_bytes + 64) & ~size_t(3);
+  EvalCtx* c = acquire_ctx(dev);
+  if (!c) return L7M_EDEVICE;
+  int rc = c->reserve(abytes, n, nctr);
+  if (rc == L7M_OK) {
+    const hipStream_t st = c->stream;
+    bool ok = hipMemsetAsync(static_cast<uint8_t*>(c->arena) + arena_bytes, 0, abytes - arena_bytes, st) == hipSuccess &&
+              hipMemcpyAsync(c->arena, arena, arena_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+              hipMemcpyAsync(c->offs, offsets, n * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+              (!hits || hipMemsetAsync(c->hits, 0, nctr * 8, st) == hipSuccess);
+    if (!ok) rc = L7M_EDEVICE;
+    if (rc == L7M_OK) rc = launch(rs, c->arena, arena_bytes, c->offs, n, c->verd, hits ? c->hits : nullptr, st, flags);
+    if (rc == L7M_OK && hipMemcpyAsync(verdicts, c->verd, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = L7M_EDEVICE;
+    if (rc == L7M_OK && hits && hipMemcpyAsync(c->hhost.data(), c->hits, nctr * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = L7M_EDEVICE;
+    if (hipStreamSynchronize(st) != hipSuccess && rc == L7M_OK) rc = L7M_EDEVICE;
+    if (rc == L7M_OK && hits)
+      for (size_t i = 0; i < nctr; ++i) hits[i] += c->hhost[i];
   }
-  bool ok = hipMemsetAsync(da, 0, abytes, st) == hipSuccess &&
-            hipMemcpyAsync(da, arena, arena_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
-            hipMemcpyAsync(doff, offsets, n * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
-            (!hits || hipMemsetAsync(dh, 0, nctr * 8, st) == hipSuccess);
-  if (!ok) rc = L7M_EDEVICE;
-  if (rc == L7M_OK) rc = launch(rs, da, arena_bytes, doff, n, dv, dh, st, flags);
-  if (rc == L7M_OK &&
-      hipMemcpyAsync(verdicts, dv, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
-    rc = L7M_EDEVICE;
-  std::vector<uint64_t> hh;
-  if (rc == L7M_OK && hits) {
-    hh.resize(nctr);
-    if (hipMemcpyAsync(hh.data(), dh, nctr * 8, hipMemcpyDeviceToHost, st) != hipSuccess) rc = L7M_EDEVICE;
-  }
-  if (hipStreamSynchronize(st) != hipSuccess && rc == L7M_OK) rc = L7M_EDEVICE;
-  if (rc == L7M_OK && hits)
-    for (size_t i = 0; i < nctr; ++i) hits[i] += hh[i];
-  cleanup();
+  release_ctx(dev, c);
   return rc;
 }
 

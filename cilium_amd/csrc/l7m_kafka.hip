@@ -16,8 +16,12 @@
 //                                     Topic==t and ruleMatches)
 //      which is the index at which the reference's ordered loop returns true
 //      (the max term is the rule that removes the last uncovered topic).
-// Verdicts: -1 deny, -2 ReadRequest error, -3 compressed message set, i >= 0
-// allowed by rule i.
+// Verdicts: -1 deny, -2 ReadRequest error, -3 a compressed message set the
+// second pass could not evaluate (queue / slab limits), i >= 0 allowed by rule i.
+// Compressed (gzip / snappy) messages: the first pass queues their values and
+// decides the request as if they decoded; kafka_codec_kernel then decodes
+// each one and re-reads the decoded set (l7m_kcodec.h) and turns the
+// request's verdict into -2 where the reference's ReadRequest would fail.
 // Records are staged through LDS per wave tile exactly like the HTTP kernel
 // (l7m_kernels.hip); the decoder then reads LDS.
 #include <hip/hip_runtime.h>
@@ -25,6 +29,7 @@
 
 #include "../../include/l7match.h"
 #include "l7m_device.h"
+#include "l7m_kcodec.h"
 #include "program.h"
 
 namespace l7m {
@@ -108,10 +113,21 @@ __device__ __forceinline__ void rd_skip_bytes(Rd& d) {
   d.pos += static_cast<uint32_t>(n);
 }
 
-enum { kMsOk = 0, kMsErr = 1, kMsUnsupported = 2 };
+enum { kMsOk = 0, kMsErr = 1 };
+
+// Where the first pass queues compressed values for kafka_codec_kernel.
+struct KPush {
+  KafkaCodecItem* items;
+  uint32_t* qhdr;        // [0] items pushed (may exceed cap), [1] second-pass work counter
+  uint32_t cap;
+  const uint8_t* rec;    // record start in the memory the decoder reads (LDS stage or HBM)
+  uint64_t rec_off;      // record start in the arena
+  uint32_t rec_idx;
+  bool overflow;         // a value did not fit the queue: verdict -3
+};
 
 // readMessageSet (messages.go:357-483) over the next `size` bytes of d.
-__device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint32_t* crc_tab) {
+__device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint32_t* crc_tab, KPush& q) {
   if (size < 0 || size > kKafkaMaxParseBuf) return kMsErr;
   const uint32_t avail = d.len - d.pos;
   Rd r{d.p + d.pos, avail < static_cast<uint32_t>(size) ? avail : static_cast<uint32_t>(size), 0, false};
@@ -143,15 +159,33 @@ __device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint
     const int comp = attr & 3;
     if (comp == 3) break;                  // `return nil, err` with err == nil
     rd_skip_bytes(m);                      // key
-    rd_skip_bytes(m);                      // value
-    if (m.err) {
+    if (comp == 0) {
+      rd_skip_bytes(m);  // value
+      if (m.err) {
+        rc = kMsErr;
+        break;
+      }
+      continue;
+    }
+    // gzip / snappy: the value (DecodeBytes) is decoded by the second pass;
+    // a nil value cannot be decompressed (gzip.NewReader / snappy.Decode fail)
+    const int32_t vn = rd_i32(m);
+    if (m.err || vn < 1 || vn > kKafkaMaxParseBuf || m.len - m.pos < static_cast<uint32_t>(vn)) {
       rc = kMsErr;
       break;
     }
-    if (comp != 0) {  // gzip / snappy: nested set not decompressed here
-      rc = kMsUnsupported;
-      break;
+    const uint32_t at = atomicAdd(q.qhdr, 1u);
+    if (at < q.cap) {
+      KafkaCodecItem it;
+      it.rec = q.rec_idx;
+      it.len = static_cast<uint32_t>(vn);
+      it.meta = kc_item_meta(q.rec_off + static_cast<uint64_t>(mb + m.pos - q.rec), static_cast<uint32_t>(comp),
+                             version);
+      q.items[at] = it;
+    } else {
+      q.overflow = true;
     }
+    m.pos += static_cast<uint32_t>(vn);
   }
   d.pos += r.pos;
   return rc;
@@ -342,7 +376,8 @@ constexpr uint32_t kTopicQ = 4;
 // kLds: rec is in the LDS stage.
 template <bool kLds>
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
-                                              uint64_t limit, const uint32_t* crc_tab, uint16_t* tq PROF_PARAM) {
+                                              uint64_t limit, const uint32_t* crc_tab, uint16_t* tq,
+                                              KPush& q PROF_PARAM) {
 #ifdef L7M_PROF
   if (kLds) g_prof_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -380,7 +415,6 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
 
     int32_t ntop = 0;
     bool ok = true;
-    int ms = kMsOk;
     uint32_t maxf = 0, nq = 0;
     auto start_topics = [&](int32_t n) { ntop = n; };
     auto topic = [&]() {
@@ -463,17 +497,11 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
           rd_skip(d, 4);  // partition
           const int32_t mss = rd_i32(d);
           if (d.err) break;
-          const int rc = read_message_set(d, mss, version, crc_tab);
-          if (rc == kMsErr) {
+          if (read_message_set(d, mss, version, crc_tab, q) == kMsErr) {
             ok = false;
             break;
           }
-          if (rc == kMsUnsupported) {
-            ms = rc;
-            break;
-          }
         }
-        if (ms != kMsOk) break;
       } else {  // 8
         for (int32_t p = 0; p < np && !d.err; ++p) {
           rd_skip(d, 4 + 8 + (version == 1 ? 8 : 0));
@@ -482,8 +510,8 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       }
     }
     if (kind == 3 && version >= 4) rd_skip(d, 1);
-    if (ms == kMsUnsupported) return L7M_VERDICT_UNSUPPORTED;
     if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
+    if (q.overflow) return L7M_VERDICT_UNSUPPORTED;
     if (kind == 10) {
       // ConsumerMetadataReq: GetTopics() is nil and ruleMatches -> true.
       first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, false, kNone);
@@ -558,7 +586,9 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
                                                              const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                              const uint64_t* __restrict__ offs, uint64_t n,
                                                              int32_t* __restrict__ verdicts,
-                                                             unsigned long long* __restrict__ hits, uint32_t stage) {
+                                                             unsigned long long* __restrict__ hits, uint32_t stage,
+                                                             KafkaCodecItem* __restrict__ citems, uint32_t* qhdr,
+                                                             uint32_t qcap) {
   extern __shared__ __align__(16) uint32_t ksmem[];
 #ifdef L7M_PROF
   uint64_t prof[5] = {0, 0, 0, 0, 0};
@@ -667,21 +697,25 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
 #endif
     if (lane < t.take) {
       bool done = false;
+      KPush q{citems, qhdr, qcap, nullptr, o, static_cast<uint32_t>(t.cur + lane), false};
       if (lane < t.k && onext - o >= 4) {
         const uint8_t* rec = stg + (o - t.base);
+        q.rec = rec;
         const uint32_t msize = (static_cast<uint32_t>(rec[0]) << 24) | (static_cast<uint32_t>(rec[1]) << 16) |
                                (static_cast<uint32_t>(rec[2]) << 8) | rec[3];
         if (kAblate == 1) {
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq PROF_ARG);
+          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, q PROF_ARG);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
+        q.rec = arena + o;
+        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, q PROF_ARG)
+                      : L7M_VERDICT_PARSE_ERROR;
       }
       verdicts[t.cur + lane] = verdict;
     }
@@ -722,12 +756,12 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
 template <int kHits, int kAblate = 0, bool kCliLds = false>
 static hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                            uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                           unsigned long long* hits, uint32_t stage) {
+                           unsigned long long* hits, uint32_t stage, const KafkaCodecQueue& cq) {
   const hipError_t e =
       set_lds_attr_once(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate, kCliLds>), kKLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate, kCliLds>), grid, dim3(kKBlock), lds, stream, dprog, arena, arena_bytes, offs,
-                     n, verdicts, hits, stage);
+  hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate, kCliLds>), grid, dim3(kKBlock), lds, stream, dprog, arena,
+                     arena_bytes, offs, n, verdicts, hits, stage, cq.items, cq.qhdr, cq.cap);
   return hipGetLastError();
 }
 
@@ -735,7 +769,7 @@ static hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint
 
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                         const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
-                        hipStream_t stream, int num_cus, uint32_t flags) {
+                        hipStream_t stream, int num_cus, uint32_t flags, const KafkaCodecQueue& cq) {
   if (n == 0) return hipSuccess;
   const uint32_t n_ctr = h.n_rules + 2;
   const int mode = !hits ? kKNoHits : (n_ctr <= kKMaxLdsCounters ? kKLdsHits : kKGlobalHits);
@@ -755,11 +789,11 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const uint32_t st = static_cast<uint32_t>(stage);
   if (flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) {
     if (flags & L7M_FLAG_DIAG_COPY_ONLY)
-      return launch_k<kKNoHits, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
-    return launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st);
+      return launch_k<kKNoHits, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq);
+    return launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq);
   }
 #define L7M_KAFKA_LAUNCH(M, C) \
-  return launch_k<M, 0, C>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st)
+  return launch_k<M, 0, C>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq)
   if (cli_lds) {
     if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, true);
     if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, true);
@@ -769,6 +803,60 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, false);
   L7M_KAFKA_LAUNCH(kKGlobalHits, false);
 #undef L7M_KAFKA_LAUNCH
+}
+
+namespace {
+
+// Second pass over the compressed values the first pass queued: one worker
+// per workgroup (lane 0; decoding is a serial bit stream), each with its own
+// slab for the decoded sets.  A value that fails turns its request's verdict
+// into -2 (ReadRequest error) once, moving its count from the verdict's
+// counter slot to slot 1; -3 when the slab or nesting limit was reached.
+__global__ __launch_bounds__(64) void kafka_codec_kernel(const uint32_t* __restrict__ prog,
+                                                         const uint8_t* __restrict__ arena,
+                                                         const KafkaCodecItem* __restrict__ items, uint32_t* qhdr,
+                                                         uint32_t qcap, int32_t* verdicts,
+                                                         unsigned long long* hits, uint8_t* slabs,
+                                                         uint64_t slab_bytes) {
+  if (threadIdx.x != 0) return;
+  const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
+  const uint32_t* crc_tab = prog + h.off_crc;
+  uint8_t* slab = slabs + static_cast<uint64_t>(blockIdx.x) * slab_bytes;
+  const uint32_t pushed = __hip_atomic_load(qhdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n = pushed < qcap ? pushed : qcap;
+  KcInflateScratch s;
+  for (uint32_t i = atomicAdd(qhdr + 1, 1u); i < n; i = atomicAdd(qhdr + 1, 1u)) {
+    const KafkaCodecItem it = items[i];
+    const int rc = kc_check_value(arena + kc_item_offset(it.meta), it.len, kc_item_codec(it.meta),
+                                  kc_item_version(it.meta), slab, static_cast<uint32_t>(slab_bytes), crc_tab, s);
+    if (rc == kCodecOk) continue;
+    const int32_t nv = rc == kCodecErr ? L7M_VERDICT_PARSE_ERROR : L7M_VERDICT_UNSUPPORTED;
+    int32_t v = __hip_atomic_load(verdicts + it.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      // an error anywhere fails the request whatever else could not be decoded
+      if (v == L7M_VERDICT_PARSE_ERROR || (v == L7M_VERDICT_UNSUPPORTED && nv == L7M_VERDICT_UNSUPPORTED)) break;
+      const int32_t prev = atomicCAS(verdicts + it.rec, v, nv);
+      if (prev == v) {
+        if (hits && v != L7M_VERDICT_UNSUPPORTED) {
+          const uint32_t slot = v >= 0 ? static_cast<uint32_t>(v) + 2u : 0u;
+          atomicAdd(hits + slot, ~0ull);  // -1
+          atomicAdd(hits + 1, 1ull);
+        }
+        break;
+      }
+      v = prev;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_kafka_codec(const uint32_t* dprog, const uint8_t* arena, int32_t* verdicts,
+                              unsigned long long* hits, hipStream_t stream, const KafkaCodecQueue& cq) {
+  if (!cq.cap || !cq.workers) return hipSuccess;
+  hipLaunchKernelGGL(kafka_codec_kernel, dim3(cq.workers), dim3(64), 0, stream, dprog, arena, cq.items, cq.qhdr, cq.cap,
+                     verdicts, hits, cq.slabs, cq.slab_bytes);
+  return hipGetLastError();
 }
 
 }  // namespace l7m

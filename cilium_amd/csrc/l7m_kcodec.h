@@ -1,0 +1,506 @@
+// l7m_kcodec.h — validation of compressed Kafka message sets (gzip, snappy):
+// the decompress-and-recurse step of optiopay's readMessageSet
+// (vendor/github.com/optiopay/kafka/proto/messages.go:441-478) as the GPU
+// runs it in the second pass of the Kafka kernel (l7m_kafka.hip).
+//
+// Only "does the reference's ReadRequest fail?" matters for the verdict, so a
+// compressed message is checked by decoding its value and parsing the decoded
+// message set (recursively) with the same rules as the outer set:
+//   gzip    Go compress/gzip Reader (multistream): header (ID, CM 8, FEXTRA,
+//           FNAME / FCOMMENT <= 511 bytes + NUL, FHCRC), raw DEFLATE
+//           (RFC 1951 with Go compress/flate's validation: complete Huffman
+//           codes except the degenerate single code and the empty tree,
+//           HLIT <= 286, HDIST <= 30, symbols 286/287 and distance codes
+//           30/31 invalid, distances within the member's output), CRC-32 and
+//           ISIZE trailer; a next member follows unless the input ends
+//           exactly there (a header cut inside FNAME / FCOMMENT also ends the
+//           stream cleanly: Go returns the raw io.EOF of ReadByte there).
+//   snappy  proto/snappy.go: the snappy-java framing ("\x82SNAPPY\0",
+//           version 1, big-endian chunk lengths) or a raw block; blocks as
+//           github.com/golang/snappy decode.go / decode_other.go.
+//           Framing the reference would index out of range on (a panic in
+//           the proxy goroutine) is reported as a parse error.
+// A decoded set larger than maxParseBufSize fails readMessageSet's size check
+// (messages.go:358), so decoding stops there with an error.  The decoded
+// bytes live in a per-worker slab: a chain of nested sets that needs more
+// than the slab reports kCodecUnsupported (L7M_VERDICT_UNSUPPORTED) instead
+// of a verdict the reference could differ from.
+//
+// The code is plain C++ usable on host and device (tests compile it for the
+// CPU to check it against the zlib-based oracle); the product runs it only on
+// the GPU.
+#pragma once
+#include <stdint.h>
+
+#include "program.h"
+
+namespace l7m {
+
+enum CodecStatus : int { kCodecOk = 0, kCodecErr = 1, kCodecUnsupported = 2 };
+enum : uint32_t { kCodecGzip = 1, kCodecSnappy = 2 };
+constexpr uint32_t kCodecMaxDepth = 8;  // nested compressed sets followed per item
+
+__host__ __device__ inline uint32_t kc_crc_update(const uint32_t* tab, uint32_t c, const uint8_t* p, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) c = tab[(c ^ p[i]) & 0xffu] ^ (c >> 8);
+  return c;
+}
+
+// LSB-first bit reader that never reads a byte before it needs one of its
+// bits (like Go's flate reader on a ByteReader), so after the final block the
+// unused bits of the last byte are dropped and the gzip trailer starts at pos.
+struct KcBits {
+  const uint8_t* p;
+  uint32_t n, pos;
+  uint32_t buf, cnt;
+};
+__host__ __device__ inline bool kc_bits(KcBits& b, uint32_t k, uint32_t* v) {
+  while (b.cnt < k) {
+    if (b.pos >= b.n) return false;
+    b.buf |= static_cast<uint32_t>(b.p[b.pos++]) << b.cnt;
+    b.cnt += 8;
+  }
+  *v = k ? b.buf & ((1u << k) - 1u) : 0u;
+  b.buf = k < 32 ? b.buf >> k : 0u;
+  b.cnt -= k;
+  return true;
+}
+
+// Canonical Huffman code (RFC 1951 §3.2.2): counts per length and symbols in
+// (length, symbol) order.
+struct KcHuff {
+  uint16_t count[16];
+  uint16_t sym[288];
+};
+// Go compress/flate huffmanDecoder.init acceptance: false = CorruptInputError.
+__host__ __device__ inline bool kc_huff_build(KcHuff& h, const uint8_t* len, uint32_t n) {
+  for (uint32_t i = 0; i < 16; ++i) h.count[i] = 0;
+  uint32_t mn = 0, mx = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t l = len[i];
+    if (!l) continue;
+    if (!mn || l < mn) mn = l;
+    if (l > mx) mx = l;
+    h.count[l]++;
+  }
+  if (mx == 0) return true;  // empty tree: fine until used
+  uint32_t code = 0;
+  for (uint32_t i = mn; i <= mx; ++i) code = (code << 1) + h.count[i];
+  if (code != (1u << mx) && !(code == 1 && mx == 1)) return false;
+  uint16_t off[16];
+  off[1] = 0;
+  for (uint32_t i = 1; i < 15; ++i) off[i + 1] = static_cast<uint16_t>(off[i] + h.count[i]);
+  for (uint32_t i = 0; i < n; ++i)
+    if (len[i]) h.sym[off[len[i]]++] = static_cast<uint16_t>(i);
+  return true;
+}
+// Next symbol, -1 on an unassigned code, -2 when the input ends.
+__host__ __device__ inline int kc_huff_decode(KcBits& b, const KcHuff& h) {
+  int code = 0, first = 0, index = 0;
+  for (int l = 1; l < 16; ++l) {
+    uint32_t bit;
+    if (!kc_bits(b, 1, &bit)) return -2;
+    code |= static_cast<int>(bit);
+    const int count = h.count[l];
+    if (code - first < count) return h.sym[index + (code - first)];
+    index += count;
+    first = (first + count) << 1;
+    code <<= 1;
+  }
+  return -1;
+}
+
+// One raw DEFLATE stream (compress/flate) appended to dst[*o, cap); history
+// may reach back to dst[hist0].  Returns kCodecOk (stream complete), kCodecErr
+// (corrupt / truncated, or output beyond max_out) or kCodecUnsupported
+// (output beyond the slab, cap < max_out).
+struct KcInflateScratch {
+  KcHuff lit, dist;
+  uint8_t lens[320];
+};
+__host__ __device__ inline int kc_inflate(KcBits& b, uint8_t* dst, uint32_t* o, uint32_t hist0, uint32_t cap,
+                                          uint32_t max_out, KcInflateScratch& s) {
+  static const uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+  const int over = cap < max_out ? kCodecUnsupported : kCodecErr;
+  for (;;) {
+    uint32_t hdr;
+    if (!kc_bits(b, 3, &hdr)) return kCodecErr;
+    const uint32_t type = hdr >> 1;
+    if (type == 0) {  // stored
+      b.buf = 0;
+      b.cnt = 0;
+      if (b.n - b.pos < 4) return kCodecErr;
+      const uint32_t ln = b.p[b.pos] | (static_cast<uint32_t>(b.p[b.pos + 1]) << 8);
+      const uint32_t nl = b.p[b.pos + 2] | (static_cast<uint32_t>(b.p[b.pos + 3]) << 8);
+      b.pos += 4;
+      if (ln != (~nl & 0xffffu)) return kCodecErr;
+      if (b.n - b.pos < ln) return kCodecErr;
+      if (ln > max_out - *o) return kCodecErr;
+      if (ln > cap - *o) return over;
+      for (uint32_t i = 0; i < ln; ++i) dst[*o + i] = b.p[b.pos + i];
+      *o += ln;
+      b.pos += ln;
+    } else if (type == 1 || type == 2) {
+      if (type == 1) {  // fixed codes
+        for (uint32_t i = 0; i < 288; ++i) s.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+        kc_huff_build(s.lit, s.lens, 288);
+        for (uint32_t i = 0; i < 32; ++i) s.lens[i] = 5;
+        kc_huff_build(s.dist, s.lens, 32);
+      } else {  // dynamic codes (flate readHuffman)
+        uint32_t hlit, hdist, hclen;
+        if (!kc_bits(b, 5, &hlit) || !kc_bits(b, 5, &hdist) || !kc_bits(b, 4, &hclen)) return kCodecErr;
+        const uint32_t nlit = hlit + 257, ndist = hdist + 1, nclen = hclen + 4;
+        if (nlit > 286 || ndist > 30) return kCodecErr;
+        uint8_t cl[19];
+        for (uint32_t i = 0; i < 19; ++i) cl[i] = 0;
+        for (uint32_t i = 0; i < nclen; ++i) {
+          uint32_t v;
+          if (!kc_bits(b, 3, &v)) return kCodecErr;
+          cl[kClOrder[i]] = static_cast<uint8_t>(v);
+        }
+        if (!kc_huff_build(s.lit, cl, 19)) return kCodecErr;
+        const uint32_t nall = nlit + ndist;
+        for (uint32_t i = 0; i < nall;) {
+          const int x = kc_huff_decode(b, s.lit);
+          if (x < 0) return kCodecErr;
+          if (x < 16) {
+            s.lens[i++] = static_cast<uint8_t>(x);
+            continue;
+          }
+          uint32_t rep, nb, v;
+          uint8_t fill = 0;
+          if (x == 16) {
+            if (i == 0) return kCodecErr;
+            rep = 3, nb = 2, fill = s.lens[i - 1];
+          } else if (x == 17) {
+            rep = 3, nb = 3;
+          } else {
+            rep = 11, nb = 7;
+          }
+          if (!kc_bits(b, nb, &v)) return kCodecErr;
+          rep += v;
+          if (i + rep > nall) return kCodecErr;
+          for (uint32_t k = 0; k < rep; ++k) s.lens[i++] = fill;
+        }
+        if (!kc_huff_build(s.lit, s.lens, nlit) || !kc_huff_build(s.dist, s.lens + nlit, ndist)) return kCodecErr;
+      }
+      for (;;) {
+        const int v = kc_huff_decode(b, s.lit);
+        if (v < 0) return kCodecErr;
+        if (v < 256) {
+          if (*o >= max_out) return kCodecErr;
+          if (*o >= cap) return over;
+          dst[(*o)++] = static_cast<uint8_t>(v);
+          continue;
+        }
+        if (v == 256) break;
+        uint32_t len, nb;
+        if (v < 265) len = v - 254, nb = 0;
+        else if (v < 269) len = v * 2 - (265 * 2 - 11), nb = 1;
+        else if (v < 273) len = v * 4 - (269 * 4 - 19), nb = 2;
+        else if (v < 277) len = v * 8 - (273 * 8 - 35), nb = 3;
+        else if (v < 281) len = v * 16 - (277 * 16 - 67), nb = 4;
+        else if (v < 285) len = v * 32 - (281 * 32 - 131), nb = 5;
+        else if (v < 286) len = 258, nb = 0;
+        else return kCodecErr;
+        uint32_t x;
+        if (nb) {
+          if (!kc_bits(b, nb, &x)) return kCodecErr;
+          len += x;
+        }
+        const int ds = kc_huff_decode(b, s.dist);
+        if (ds < 0) return kCodecErr;
+        uint32_t dist;
+        if (ds < 4) {
+          dist = static_cast<uint32_t>(ds) + 1;
+        } else if (ds < 30) {
+          const uint32_t dnb = (static_cast<uint32_t>(ds) - 2) >> 1;
+          if (!kc_bits(b, dnb, &x)) return kCodecErr;
+          dist = (1u << (dnb + 1)) + 1 + (((static_cast<uint32_t>(ds) & 1u) << dnb) | x);
+        } else {
+          return kCodecErr;
+        }
+        if (dist > *o - hist0) return kCodecErr;
+        if (len > max_out - *o) return kCodecErr;
+        if (len > cap - *o) return over;
+        for (uint32_t k = 0; k < len; ++k, ++*o) dst[*o] = dst[*o - dist];
+      }
+    } else {
+      return kCodecErr;  // reserved block type
+    }
+    if (hdr & 1) return kCodecOk;  // BFINAL
+  }
+}
+
+// gzip member header (Go gzip.Reader.readHeader).  kCodecOk, kCodecErr, or
+// 3 = io.EOF (clean end of a multistream; an error for the first member).
+__host__ __device__ inline int kc_gzip_header(const uint8_t* p, uint32_t n, uint32_t* pos, const uint32_t* crc_tab) {
+  const uint32_t start = *pos;
+  const uint32_t rem = n - start;
+  if (rem == 0) return 3;
+  if (rem < 10) return kCodecErr;                                   // ErrUnexpectedEOF
+  if (p[start] != 0x1f || p[start + 1] != 0x8b || p[start + 2] != 8) return kCodecErr;  // ErrHeader
+  const uint32_t flg = p[start + 3];
+  uint32_t q = start + 10;
+  if (flg & 4) {  // FEXTRA
+    if (n - q < 2) return kCodecErr;
+    const uint32_t xlen = p[q] | (static_cast<uint32_t>(p[q + 1]) << 8);
+    q += 2;
+    if (n - q < xlen) return kCodecErr;
+    q += xlen;
+  }
+  for (uint32_t f = 8; f <= 16; f <<= 1) {  // FNAME, FCOMMENT: NUL-terminated, <= 512 bytes
+    if (!(flg & f)) continue;
+    for (uint32_t i = 0;; ++i) {
+      if (i >= 512) return kCodecErr;
+      if (q >= n) return 3;  // raw io.EOF from ReadByte
+      if (p[q++] == 0) break;
+    }
+  }
+  if (flg & 2) {  // FHCRC: low 16 bits of the header's CRC-32
+    if (n - q < 2) return kCodecErr;
+    const uint32_t c = kc_crc_update(crc_tab, 0xffffffffu, p + start, q - start) ^ 0xffffffffu;
+    if ((p[q] | (static_cast<uint32_t>(p[q + 1]) << 8)) != (c & 0xffffu)) return kCodecErr;
+    q += 2;
+  }
+  *pos = q;
+  return kCodecOk;
+}
+
+// gzip.NewReader + ioutil.ReadAll over src[0, n) into dst (*out bytes).
+__host__ __device__ inline int kc_gunzip(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
+                                         uint32_t max_out, uint32_t* out, const uint32_t* crc_tab,
+                                         KcInflateScratch& s) {
+  uint32_t pos = 0, o = 0;
+  int h = kc_gzip_header(src, n, &pos, crc_tab);
+  if (h != kCodecOk) return kCodecErr;
+  for (;;) {
+    KcBits b{src, n, pos, 0, 0};
+    const uint32_t o0 = o;
+    const int rc = kc_inflate(b, dst, &o, o0, cap, max_out, s);
+    if (rc != kCodecOk) return rc;
+    pos = b.pos;
+    if (n - pos < 8) return kCodecErr;
+    const uint32_t crc = kc_crc_update(crc_tab, 0xffffffffu, dst + o0, o - o0) ^ 0xffffffffu;
+    const uint32_t want_crc = src[pos] | (static_cast<uint32_t>(src[pos + 1]) << 8) |
+                              (static_cast<uint32_t>(src[pos + 2]) << 16) | (static_cast<uint32_t>(src[pos + 3]) << 24);
+    const uint32_t want_len = src[pos + 4] | (static_cast<uint32_t>(src[pos + 5]) << 8) |
+                              (static_cast<uint32_t>(src[pos + 6]) << 16) | (static_cast<uint32_t>(src[pos + 7]) << 24);
+    if (crc != want_crc || (o - o0) != want_len) return kCodecErr;  // ErrChecksum
+    pos += 8;
+    h = kc_gzip_header(src, n, &pos, crc_tab);
+    if (h == 3) break;
+    if (h != kCodecOk) return kCodecErr;
+  }
+  *out = o;
+  return kCodecOk;
+}
+
+// github.com/golang/snappy Decode of one block src[0, n) appended at dst[*o].
+__host__ __device__ inline int kc_snappy_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t* o,
+                                               uint32_t cap, uint32_t max_out) {
+  // binary.Uvarint
+  uint64_t v = 0;
+  uint32_t s = 0, hl = 0;
+  bool done = false;
+  for (uint32_t i = 0; i < n && i < 10; ++i) {
+    const uint8_t c = src[i];
+    if (c < 0x80) {
+      if (i == 9 && c > 1) return kCodecErr;  // overflow
+      v |= static_cast<uint64_t>(c) << s;
+      hl = i + 1;
+      done = true;
+      break;
+    }
+    v |= static_cast<uint64_t>(c & 0x7f) << s;
+    s += 7;
+  }
+  if (!done || v > 0xffffffffull) return kCodecErr;
+  if (v > max_out - *o) return kCodecErr;  // the decoded set cannot pass readMessageSet
+  if (v > cap - *o) return kCodecUnsupported;
+  const uint32_t dlen = static_cast<uint32_t>(v);
+  uint8_t* d0 = dst + *o;
+  uint32_t d = 0, p = hl;
+  while (p < n) {
+    const uint32_t tag = src[p] & 3u;
+    uint32_t length, offset;
+    if (tag == 0) {  // literal
+      uint32_t x = src[p] >> 2;
+      if (x < 60) {
+        p += 1;
+      } else {
+        const uint32_t k = x - 59;  // 1..4 length bytes
+        if (n - p < k + 1) return kCodecErr;
+        x = 0;
+        for (uint32_t i = 0; i < k; ++i) x |= static_cast<uint32_t>(src[p + 1 + i]) << (8 * i);
+        p += 1 + k;
+      }
+      const uint64_t ln = static_cast<uint64_t>(x) + 1;
+      if (ln > dlen - d || ln > n - p) return kCodecErr;
+      for (uint32_t i = 0; i < ln; ++i) d0[d + i] = src[p + i];
+      d += static_cast<uint32_t>(ln);
+      p += static_cast<uint32_t>(ln);
+      continue;
+    }
+    if (tag == 1) {
+      if (n - p < 2) return kCodecErr;
+      length = 4 + ((src[p] >> 2) & 7u);
+      offset = ((src[p] & 0xe0u) << 3) | src[p + 1];
+      p += 2;
+    } else if (tag == 2) {
+      if (n - p < 3) return kCodecErr;
+      length = 1 + (src[p] >> 2);
+      offset = src[p + 1] | (static_cast<uint32_t>(src[p + 2]) << 8);
+      p += 3;
+    } else {
+      if (n - p < 5) return kCodecErr;
+      length = 1 + (src[p] >> 2);
+      offset = src[p + 1] | (static_cast<uint32_t>(src[p + 2]) << 8) | (static_cast<uint32_t>(src[p + 3]) << 16) |
+               (static_cast<uint32_t>(src[p + 4]) << 24);
+      p += 5;
+    }
+    // int(uint32) on a 64-bit Go: offsets >= 2^31 stay positive
+    if (offset == 0 || d < offset || length > dlen - d) return kCodecErr;
+    for (uint32_t end = d + length; d != end; ++d) d0[d] = d0[d - offset];
+  }
+  if (d != dlen) return kCodecErr;
+  *o += dlen;
+  return kCodecOk;
+}
+
+// proto/snappy.go snappyDecode.
+__host__ __device__ inline int kc_unsnappy(const uint8_t* b, uint32_t n, uint8_t* dst, uint32_t cap, uint32_t max_out,
+                                           uint32_t* out) {
+  static const uint8_t kMagic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
+  bool framed = n >= 8;
+  for (uint32_t i = 0; i < 8 && framed; ++i) framed = b[i] == kMagic[i];
+  uint32_t o = 0;
+  if (!framed) {
+    const int rc = kc_snappy_block(b, n, dst, &o, cap, max_out);
+    *out = o;
+    return rc;
+  }
+  if (n < 12) return kCodecErr;  // b[8:12] out of range: the reference panics
+  const uint32_t ver = (static_cast<uint32_t>(b[8]) << 24) | (static_cast<uint32_t>(b[9]) << 16) |
+                       (static_cast<uint32_t>(b[10]) << 8) | b[11];
+  if (ver != 1) return kCodecErr;
+  for (uint32_t i = 16; i < n;) {
+    if (n - i < 4) return kCodecErr;  // b[i:i+4] out of range
+    const uint32_t cl = (static_cast<uint32_t>(b[i]) << 24) | (static_cast<uint32_t>(b[i + 1]) << 16) |
+                        (static_cast<uint32_t>(b[i + 2]) << 8) | b[i + 3];
+    i += 4;
+    if (cl > n - i) return kCodecErr;  // b[i:i+n] out of range
+    const int rc = kc_snappy_block(b + i, cl, dst, &o, cap, max_out);
+    if (rc != kCodecOk) return rc;
+    i += cl;
+  }
+  *out = o;
+  return kCodecOk;
+}
+
+// ---- readMessageSet over decoded bytes, following nested compression -----
+struct KcRd {
+  const uint8_t* p;
+  uint32_t len, pos;
+  bool err;
+};
+__host__ __device__ inline uint64_t kc_be(KcRd& d, uint32_t k) {
+  if (d.err) return 0;
+  if (d.len - d.pos < k) {
+    d.pos = d.len;
+    d.err = true;
+    return 0;
+  }
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < k; ++i) v = (v << 8) | d.p[d.pos + i];
+  d.pos += k;
+  return v;
+}
+// DecodeBytes (serialization.go:165-192): data offset / length (0 = nil).
+__host__ __device__ inline void kc_bytes(KcRd& d, uint32_t* off, uint32_t* len) {
+  *off = 0;
+  *len = 0;
+  if (d.err) return;
+  const int32_t n = static_cast<int32_t>(kc_be(d, 4));
+  if (d.err || n < 1) return;
+  if (n > kKafkaMaxParseBuf || d.len - d.pos < static_cast<uint32_t>(n)) {
+    d.pos = d.len;
+    d.err = true;
+    return;
+  }
+  *off = d.pos;
+  *len = static_cast<uint32_t>(n);
+  d.pos += static_cast<uint32_t>(n);
+}
+
+struct KcFrame {
+  const uint8_t* p;
+  uint32_t len, pos, slab_top;
+};
+
+// Decode one compressed value into slab[top, ...) and check the decoded set
+// (and every compressed set nested in it) as readMessageSet would.
+__host__ __device__ inline int kc_check_value(const uint8_t* val, uint32_t vlen, uint32_t codec, int16_t version,
+                                              uint8_t* slab, uint32_t slab_bytes, const uint32_t* crc_tab,
+                                              KcInflateScratch& s) {
+  KcFrame st[kCodecMaxDepth];
+  uint32_t sp = 0, top = 0;
+  const uint32_t max_out = static_cast<uint32_t>(kKafkaMaxParseBuf);
+  auto decode = [&](const uint8_t* src, uint32_t n, uint32_t cdc) -> int {
+    if (sp >= kCodecMaxDepth) return kCodecUnsupported;
+    uint32_t out = 0;
+    const uint32_t cap = slab_bytes - top;
+    const int rc = cdc == kCodecGzip ? kc_gunzip(src, n, slab + top, cap, max_out, &out, crc_tab, s)
+                                     : kc_unsnappy(src, n, slab + top, cap, max_out, &out);
+    if (rc != kCodecOk) return rc;
+    st[sp++] = KcFrame{slab + top, out, 0, top};
+    top += out;
+    return kCodecOk;
+  };
+  int rc = decode(val, vlen, codec);
+  while (rc == kCodecOk && sp > 0) {
+    KcFrame& f = st[sp - 1];
+    KcRd r{f.p, f.len, f.pos, false};
+    bool pop = false;
+    kc_be(r, 8);  // offset
+    const int32_t msz = static_cast<int32_t>(kc_be(r, 4));
+    if (r.err || msz <= 0) {
+      pop = true;  // EOF / empty message: end of the set
+    } else if (msz > kKafkaMaxParseBuf) {
+      rc = kCodecErr;  // allocParseBuf
+    } else if (r.len - r.pos < static_cast<uint32_t>(msz)) {
+      pop = true;  // truncated last message is ignored
+    } else {
+      const uint8_t* mb = r.p + r.pos;
+      r.pos += static_cast<uint32_t>(msz);
+      f.pos = r.pos;
+      KcRd m{mb, static_cast<uint32_t>(msz), 0, false};
+      const uint32_t crc = static_cast<uint32_t>(kc_be(m, 4));
+      if (msz <= 4) {
+        pop = true;
+      } else if (crc != (kc_crc_update(crc_tab, 0xffffffffu, mb + 4, static_cast<uint32_t>(msz) - 4) ^ 0xffffffffu)) {
+        pop = true;  // ignore the rest of the set
+      } else {
+        kc_be(m, 1);  // magic
+        const uint32_t attr = static_cast<uint32_t>(kc_be(m, 1));
+        if (version >= 1) kc_be(m, 8);  // timestamp
+        const uint32_t comp = attr & 3u;
+        uint32_t ko, kl, vo, vl;
+        if (comp == 3) {
+          pop = true;  // `return nil, err` with a nil err: the set ends without error
+        } else {
+          kc_bytes(m, &ko, &kl);
+          kc_bytes(m, &vo, &vl);
+          if (m.err) rc = kCodecErr;
+          else if (comp != 0) rc = decode(mb + vo, vl, comp);
+        }
+      }
+    }
+    if (pop) {
+      top = st[sp - 1].slab_top;
+      --sp;
+    }
+  }
+  return rc;
+}
+
+}  // namespace l7m

@@ -29,6 +29,9 @@
 //                          (messages.go:357-482, 493-522, 752-809, 1018-1039,
 //                          1158-1213, 1374-1411, 1572-1628, 1791-1839),
 //                          decoder semantics serialization.go:30-196, utils.go:9-24
+//   compressed sets        messages.go:441-478: gzip (Go compress/gzip framing restated,
+//                          DEFLATE by zlib), snappy (github.com/golang/snappy decode.go,
+//                          proto/snappy.go), decoded sets read recursively
 //   MatchesRule            pkg/kafka/policy.go:27-225
 // Verdict encoding matches include/l7match.h (-1 deny, i >= 0 deciding rule).
 #include <algorithm>
@@ -42,6 +45,8 @@
 #include <thread>
 #include <unordered_set>
 #include <vector>
+
+#include <zlib.h>
 
 #include "../include/l7match.h"
 
@@ -460,7 +465,169 @@ uint32_t crc32_ieee(const uint8_t* p, size_t n) {
 
 enum MsRc { MS_OK, MS_ERR, MS_UNSUPPORTED };
 
-// readMessageSet(r, size, version): reads at most `size` bytes of `outer`.
+// ---- compressed message sets (messages.go:441-478) -------------------------
+// gzip.NewReader + ioutil.ReadAll (Go compress/gzip, multistream): the member
+// framing restated here, the DEFLATE data inflated by zlib (raw mode) — an
+// implementation independent of the product's device decoder.  A decoded
+// size above maxParseBufSize fails readMessageSet's size check, so inflating
+// stops there with an error.  Returns true on success.
+bool go_gunzip(const std::string& in, std::vector<uint8_t>* out) {
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(in.data());
+  const size_t n = in.size();
+  size_t pos = 0;
+  auto header = [&]() -> int {  // 0 ok, 1 error, 2 io.EOF
+    const size_t rem = n - pos;
+    if (rem == 0) return 2;                                        // ReadFull: EOF
+    if (rem < 10) return 1;                                        // ErrUnexpectedEOF
+    if (p[pos] != 0x1f || p[pos + 1] != 0x8b || p[pos + 2] != 8) return 1;  // ErrHeader
+    const uint8_t flg = p[pos + 3];
+    size_t q = pos + 10;
+    if (flg & 0x04) {  // FEXTRA
+      if (n - q < 2) return 1;
+      const size_t xl = p[q] | (p[q + 1] << 8);
+      q += 2;
+      if (n - q < xl) return 1;
+      q += xl;
+    }
+    for (int f : {0x08, 0x10}) {  // FNAME, FCOMMENT (readString: z.buf is 512 bytes)
+      if (!(flg & f)) continue;
+      for (int i = 0;; ++i) {
+        if (i >= 512) return 1;
+        if (q >= n) return 2;  // ReadByte's io.EOF is returned as is
+        if (p[q++] == 0) break;
+      }
+    }
+    if (flg & 0x02) {  // FHCRC
+      if (n - q < 2) return 1;
+      const uint32_t c = static_cast<uint32_t>(crc32(0L, p + pos, static_cast<uInt>(q - pos)));
+      if ((p[q] | (p[q + 1] << 8)) != (c & 0xffff)) return 1;
+      q += 2;
+    }
+    pos = q;
+    return 0;
+  };
+  if (header() != 0) return false;  // NewReader fails, io.EOF included
+  for (;;) {
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return false;
+    zs.next_in = const_cast<Bytef*>(p + pos);
+    zs.avail_in = static_cast<uInt>(n - pos);
+    const size_t start = out->size();
+    std::vector<uint8_t> buf(1 << 16);
+    int rc;
+    do {
+      zs.next_out = buf.data();
+      zs.avail_out = static_cast<uInt>(buf.size());
+      rc = inflate(&zs, Z_NO_FLUSH);
+      out->insert(out->end(), buf.data(), buf.data() + (buf.size() - zs.avail_out));
+      if (out->size() > static_cast<size_t>(kMaxParseBuf)) rc = Z_DATA_ERROR;
+    } while (rc == Z_OK);
+    const size_t left = zs.avail_in;
+    inflateEnd(&zs);
+    if (rc != Z_STREAM_END) return false;
+    pos = n - left;
+    if (n - pos < 8) return false;
+    const uint32_t c = static_cast<uint32_t>(crc32(0L, out->data() + start, static_cast<uInt>(out->size() - start)));
+    const uint32_t wc = p[pos] | (p[pos + 1] << 8) | (p[pos + 2] << 16) | ((uint32_t)p[pos + 3] << 24);
+    const uint32_t wl = p[pos + 4] | (p[pos + 5] << 8) | (p[pos + 6] << 16) | ((uint32_t)p[pos + 7] << 24);
+    if (c != wc || static_cast<uint32_t>(out->size() - start) != wl) return false;  // ErrChecksum
+    pos += 8;
+    const int h = header();
+    if (h == 2) return true;
+    if (h == 1) return false;
+  }
+}
+
+// github.com/golang/snappy Decode (decode.go:25-72, decode_other.go:14-102).
+bool go_snappy_block(const uint8_t* src, size_t n, std::vector<uint8_t>* out) {
+  uint64_t v = 0;
+  unsigned shift = 0;
+  size_t hl = 0;
+  for (size_t i = 0;; ++i) {  // binary.Uvarint
+    if (i >= n) return false;
+    const uint8_t b = src[i];
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) return false;
+      v |= (uint64_t)b << shift;
+      hl = i + 1;
+      break;
+    }
+    v |= (uint64_t)(b & 0x7f) << shift;
+    shift += 7;
+  }
+  if (v > 0xffffffffull) return false;
+  if (out->size() + v > static_cast<uint64_t>(kMaxParseBuf)) return false;  // the set cannot pass readMessageSet
+  const size_t base = out->size();
+  out->resize(base + v);
+  uint8_t* dst = out->data() + base;
+  const int64_t dlen = (int64_t)v;
+  int64_t d = 0, s = (int64_t)hl, len = (int64_t)n, length = 0, offset = 0;
+  while (s < len) {
+    const int tag = src[s] & 3;
+    if (tag == 0) {
+      uint32_t x = src[s] >> 2;
+      if (x < 60) {
+        s++;
+      } else {
+        const int k = (int)x - 59;
+        s += 1 + k;
+        if (s > len) return false;
+        x = 0;
+        for (int i = 0; i < k; ++i) x |= (uint32_t)src[s - k + i] << (8 * i);
+      }
+      length = (int64_t)x + 1;
+      if (length > dlen - d || length > len - s) return false;
+      memcpy(dst + d, src + s, (size_t)length);
+      d += length;
+      s += length;
+      continue;
+    } else if (tag == 1) {
+      s += 2;
+      if (s > len) return false;
+      length = 4 + ((src[s - 2] >> 2) & 7);
+      offset = ((src[s - 2] & 0xe0) << 3) | src[s - 1];
+    } else if (tag == 2) {
+      s += 3;
+      if (s > len) return false;
+      length = 1 + (src[s - 3] >> 2);
+      offset = src[s - 2] | (src[s - 1] << 8);
+    } else {
+      s += 5;
+      if (s > len) return false;
+      length = 1 + (src[s - 5] >> 2);
+      offset = (int64_t)((uint32_t)src[s - 4] | ((uint32_t)src[s - 3] << 8) | ((uint32_t)src[s - 2] << 16) |
+                         ((uint32_t)src[s - 1] << 24));
+    }
+    if (offset <= 0 || d < offset || length > dlen - d) return false;
+    for (int64_t end = d + length; d != end; ++d) dst[d] = dst[d - offset];
+  }
+  return d == dlen;
+}
+
+// proto/snappy.go snappyDecode; its out-of-range slicing on short snappy-java
+// framing panics in the reference — reported here as an error.
+bool go_snappy(const std::string& in, std::vector<uint8_t>* out) {
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(in.data());
+  const size_t n = in.size();
+  static const uint8_t magic[8] = {0x82, 'S', 'N', 'A', 'P', 'P', 'Y', 0};
+  if (n < 8 || memcmp(b, magic, 8) != 0) return go_snappy_block(b, n, out);
+  if (n < 12) return false;
+  const uint32_t ver = ((uint32_t)b[8] << 24) | (b[9] << 16) | (b[10] << 8) | b[11];
+  if (ver != 1) return false;
+  for (size_t i = 16; i < n;) {
+    if (n - i < 4) return false;
+    const size_t cl = ((uint32_t)b[i] << 24) | (b[i + 1] << 16) | (b[i + 2] << 8) | b[i + 3];
+    i += 4;
+    if (cl > n - i) return false;
+    if (!go_snappy_block(b + i, cl, out)) return false;
+    i += cl;
+  }
+  return true;
+}
+
+// readMessageSet(r, size, version): reads at most `size` bytes of `outer`,
+// decompressing gzip / snappy messages and reading their sets recursively.
 MsRc read_message_set(Reader* outer, int32_t size, int16_t version) {
   if (size < 0 || size > kMaxParseBuf) return MS_ERR;
   size_t lim = outer->avail() < (size_t)size ? outer->avail() : (size_t)size;
@@ -491,11 +658,15 @@ MsRc read_message_set(Reader* outer, int32_t size, int16_t version) {
       md.bytes(nullptr);
       if (md.err) { done(); return MS_ERR; }
     } else if (comp == 1 || comp == 2) {
-      md.bytes(nullptr);
-      md.bytes(nullptr);
+      md.bytes(nullptr);  // key ignored
+      std::string val;
+      md.bytes(&val);     // nil for a length < 1
       if (md.err) { done(); return MS_ERR; }
-      done();
-      return MS_UNSUPPORTED;  // gzip / snappy payload: not evaluated
+      std::vector<uint8_t> decoded;
+      const bool ok = comp == 1 ? go_gunzip(val, &decoded) : go_snappy(val, &decoded);
+      if (!ok || decoded.size() > (size_t)kMaxParseBuf) { done(); return MS_ERR; }
+      Reader in{decoded.data(), decoded.size(), 0};
+      if (read_message_set(&in, (int32_t)decoded.size(), version) == MS_ERR) { done(); return MS_ERR; }
     } else {
       done();
       return MS_OK;  // `return nil, err` with err == nil (messages.go:479-480)

@@ -184,3 +184,95 @@ def mutate(rng, rec: bytes) -> bytes:
         r += bytes(rng.integers(0, 256, size=int(rng.integers(1, 9)), dtype="uint8"))
         r[0:4] = struct.pack(">i", len(r) - 4)
     return bytes(r)
+
+
+# ---- compressed message sets (messages.go:441-478) ------------------------
+GZIP, SNAPPY = 1, 2
+
+
+def gzip_member(data, level=6, fname=None, fcomment=None, fextra=None, fhcrc=False, strategy=None):
+    """One gzip member (RFC 1952) with the optional header fields Go's
+    gzip.Reader parses; DEFLATE data from zlib (raw)."""
+    flg = (4 if fextra is not None else 0) | (8 if fname is not None else 0) | \
+          (16 if fcomment is not None else 0) | (2 if fhcrc else 0)
+    hdr = bytes([0x1F, 0x8B, 8, flg]) + struct.pack("<I", 0) + bytes([0, 255])
+    if fextra is not None:
+        hdr += struct.pack("<H", len(fextra)) + fextra
+    if fname is not None:
+        hdr += fname + b"\0"
+    if fcomment is not None:
+        hdr += fcomment + b"\0"
+    if fhcrc:
+        hdr += struct.pack("<H", zlib.crc32(hdr) & 0xFFFF)
+    co = zlib.compressobj(level, zlib.DEFLATED, -15, 8, strategy if strategy is not None else zlib.Z_DEFAULT_STRATEGY)
+    body = co.compress(data) + co.flush()
+    return hdr + body + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data) & 0xFFFFFFFF)
+
+
+def _uvarint(n):
+    out = b""
+    while n >= 0x80:
+        out += bytes([(n & 0x7F) | 0x80])
+        n >>= 7
+    return out + bytes([n])
+
+
+def snappy_block(data):
+    """A valid snappy block (github.com/golang/snappy format): greedy 4-byte
+    hash matches as copy-2 elements, literals otherwise."""
+    out = bytearray(_uvarint(len(data)))
+    table, i, lit = {}, 0, 0
+
+    def emit_literal(a, b):
+        n = b - a
+        while n > 0:
+            k = min(n, 1 << 16)
+            if k - 1 < 60:
+                out.append((k - 1) << 2)
+            elif k - 1 < 256:
+                out.extend([60 << 2, k - 1])
+            else:
+                out.extend([61 << 2, (k - 1) & 0xFF, (k - 1) >> 8])
+            out.extend(data[a:a + k])
+            a += k
+            n -= k
+
+    while i + 4 <= len(data):
+        key = bytes(data[i:i + 4])
+        j = table.get(key)
+        table[key] = i
+        if j is not None and i - j < 65536:
+            m = 4
+            while i + m < len(data) and data[j + m] == data[i + m] and m < 64:
+                m += 1
+            emit_literal(lit, i)
+            out.extend([((m - 1) << 2) | 2, (i - j) & 0xFF, (i - j) >> 8])
+            i += m
+            lit = i
+        else:
+            i += 1
+    emit_literal(lit, len(data))
+    return bytes(out)
+
+
+def snappy_java(data, chunk=1024, version=1):
+    """snappy-java framing (proto/snappy.go): magic, version, compat, chunks."""
+    out = b"\x82SNAPPY\x00" + struct.pack(">II", version, 1)
+    for k in range(0, len(data), chunk):
+        blk = snappy_block(data[k:k + chunk])
+        out += struct.pack(">I", len(blk)) + blk
+    return out
+
+
+def wrapper_set(value, codec, version=0, bad_crc=False):
+    """A message set holding ONE compressed message whose value is `value`
+    (already compressed bytes), attributes = codec."""
+    body = struct.pack(">bb", 0, codec)
+    if version >= 1:
+        body += struct.pack(">q", 1_500_000_000_000)
+    body += b(None) + b(value)
+    crc = zlib.crc32(body) & 0xFFFFFFFF
+    if bad_crc:
+        crc ^= 1
+    m = struct.pack(">I", crc) + body
+    return struct.pack(">qi", 0, len(m)) + m

@@ -75,12 +75,12 @@ def test_oracle_message_set_semantics():
     ms_attr3 = K.message_set(["zz"], version=1, compression=3)
     recs = [K.produce(0, "c", [("t", [(0, ms_ok)])]),
             K.produce(0, "c", [("t", [(0, ms_badcrc)])]),       # CRC mismatch: rest of set left unread
-            K.produce(1, "c", [("t", [(0, ms_gzip)])]),         # compressed: not evaluated
+            K.produce(1, "c", [("t", [(0, ms_gzip)])]),         # "zz" is no gzip stream: NewReader fails
             K.produce(1, "c", [("t", [(0, ms_attr3)])]),        # attribute 3: nil, nil
             K.produce(0, "c", [("t", [(0, ms_ok[:-3])])])]      # truncated last message: ignored
     arena, offs = L.pack_records(recs)
     v = KafkaOracle([L.PortRuleKafka(Topic="t")]).eval(arena, offs)
-    assert v.tolist() == [0, 0, L.VERDICT_UNSUPPORTED, 0, 0]
+    assert v.tolist() == [0, 0, L.VERDICT_PARSE_ERROR, 0, 0]
 
 
 def test_config3_generator_and_oracle_sample():
