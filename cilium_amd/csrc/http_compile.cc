@@ -589,6 +589,24 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   h.any_remotes = any_remotes ? 1u : 0u;
   h.zero_list = zero_span;
   h.single_entry = plan.single ? 1u : 0u;
+  {
+    // the pseudo-header DFA most rules are keyed on: its candidate entry is
+    // fetched as soon as its walk ends, hiding the L2 latency behind the rest
+    h.pf_dfa = kNone;
+    size_t most = 0;
+    for (uint32_t f = 0; f < 3 && f < nf; ++f)
+      for (uint32_t g = 0; g < groups[f].size(); ++g) {
+        size_t k = 0;
+        for (const auto& kl : keyed[dfa_first[f] + g]) k += kl.size();
+        if (k > most) most = k, h.pf_dfa = dfa_first[f] + g;
+      }
+  }
+  {
+    uint64_t m = 0;
+    for (uint32_t f = 3; f < nf; ++f) m |= 1ull << std::min<size_t>(field_names[f].size(), 63);
+    h.name_len_lo = static_cast<uint32_t>(m);
+    h.name_len_hi = static_cast<uint32_t>(m >> 32);
+  }
   h.n_policies = plan.n_policies;
   h.ent_mask = ent_slots - 1;
   h.ent_tab_off = take(2ull * ent_slots);

@@ -174,7 +174,12 @@ __device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint
       rc = kMsErr;
       break;
     }
+#ifdef L7M_NO_CODEC_QUEUE  // A/B diagnostic build: no second pass, compressed = unsupported
+    q.overflow = true;
+    const uint32_t at = q.cap;
+#else
     const uint32_t at = atomicAdd(q.qhdr, 1u);
+#endif
     if (at < q.cap) {
       KafkaCodecItem it;
       it.rec = q.rec_idx;

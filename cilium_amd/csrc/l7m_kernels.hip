@@ -327,11 +327,28 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   uint64_t present = 0;
   codes.clear(h.n_dfas);
   uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
+  // Candidate entry of the prefetch DFA (h.pf_dfa), loaded as soon as its
+  // walk ends so that the L2 latency overlaps the remaining walks.
+  u32x4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0}, pf2 = {0, 0, 0, 0};
+  auto prefetch = [&](uint32_t d, uint32_t code) {
+    if (!code) return;
+    const DfaDesc& dd = c.dds[d];
+    const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
+    const uint32_t mw = dd.lds_ctmask != kNone ? c.img[dd.lds_ctmask + (idx >> 5)] : c.prog[dd.ctmask_off + (idx >> 5)];
+    if (!((mw >> (idx & 31u)) & 1u)) return;
+    const u32x4* e = reinterpret_cast<const u32x4*>(dd.lds_ct != kNone ? c.img + dd.lds_ct + 16u * idx
+                                                                       : c.prog + dd.ct_off + 16u * idx);
+    pf0 = e[0];
+    pf1 = e[1];
+    pf2 = e[2];
+  };
   auto eval_field = [&](uint32_t f, uint32_t p, uint32_t len) {
     const FieldDesc& fd = c.fields[f];
     for (uint32_t k = 0; k < fd.ndfa; ++k) {
       const uint32_t d = fd.dfa_first + k;
-      codes.set(d, walk_dfa(c, d, src, p, len));
+      const uint32_t code = walk_dfa(c, d, src, p, len);
+      codes.set(d, code);
+      if (d == h.pf_dfa) prefetch(d, code);
     }
   };
   if (flags & L7M_HTTP_F_METHOD) {
@@ -357,7 +374,10 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
       const uint32_t e = src.word(5 + j);
       const uint32_t nl = e & 0xffffu, vl = e >> 16;
       uint32_t f = kNone;
-      if (h.lds_name_tab != kNone) {
+      const uint32_t lb = nl < 63 ? nl : 63;
+      if (!(((lb < 32 ? h.name_len_lo >> lb : h.name_len_hi >> (lb - 32)) & 1u))) {
+        // no rule references a header name of this length
+      } else if (h.lds_name_tab != kNone) {
         f = name_field_of(c, h, src, pos, nl);
       } else {
         const uint32_t code = walk_dfa(c, h.n_dfas, src, pos, nl);
@@ -418,13 +438,10 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   };
   // Candidates of each DFA end code: one 64-byte CandEntry whose first check
   // record is inline; longer lists fall back to the pool scan.
-  auto check_inline = [&](const uint32_t* e) {  // e -> CandEntry (LDS or HBM)
-    const u32x4 q0 = reinterpret_cast<const u32x4*>(e)[0];  // len, off, rid, hdr
-    const uint32_t len = q0.x, rid = q0.z, hd = q0.w, nm = cr_matchers(hd);
+  auto check_entry = [&](const u32x4 q0, const u32x4 q1, const u32x4 q2) {  // a CandEntry's first 48 bytes
+    const uint32_t len = q0.x, rid = q0.z, hd = q0.w, nm = cr_matchers(hd);  // len, off, rid, hdr
     if (len == 1 && nm <= kCandInlineMatchers) {
       if (rid >= best) return;
-      const u32x4 q1 = reinterpret_cast<const u32x4*>(e)[1];
-      const u32x4 q2 = reinterpret_cast<const u32x4*>(e)[2];
       const uint32_t ma[4] = {q1.x, q1.z, q2.x, q2.z}, mp[4] = {q1.y, q1.w, q2.y, q2.w};
       bool ok = eligible(hd) && (!(hd & kCrRemote) || remote_ok(rid));
 #pragma unroll
@@ -440,9 +457,14 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
       scan(Span{q0.y, len});
     }
   };
+  auto check_inline = [&](const uint32_t* e) {  // e -> CandEntry (LDS or HBM)
+    const u32x4* q = reinterpret_cast<const u32x4*>(e);
+    check_entry(q[0], q[1], q[2]);
+  };
+  if (h.pf_dfa != kNone && pf0.x) check_entry(pf0, pf1, pf2);
   for (uint32_t d = 0; d < h.n_dfas; ++d) {
     const uint32_t code = codes.get(d);
-    if (!code) continue;
+    if (!code || d == h.pf_dfa) continue;
     const DfaDesc& dd = c.dds[d];
     const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
     const uint32_t mw = dd.lds_ctmask != kNone ? c.img[dd.lds_ctmask + (idx >> 5)] : c.prog[dd.ctmask_off + (idx >> 5)];
@@ -610,7 +632,8 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
 #endif
     if (kHits != kNoHits) {
       uint32_t slot = kNone;
-      if (lane < take && v != L7M_VERDICT_ALLOW_NO_L7)
+      // allows decided without a rule (no L7 rules, no port policy) are not counted
+      if (lane < take && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY)
         slot = v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u);
       if (kHits == kLdsHits) {
         if (slot != kNone) atomicAdd(ctr + slot, 1u);

@@ -157,14 +157,18 @@ struct HttpHeader {
   uint32_t ent_tab_off;    // program: port-entry table
   uint32_t lds_ent_tab;    // LDS image copy, or kNone
   uint32_t ent_mask;       // its slot count - 1
-  uint32_t pad[2];         // header = 32 words
+  uint32_t name_len_lo;    // bit l (l < 64, 63 = longer) set iff a referenced header
+  uint32_t name_len_hi;    // name has that length: other names skip the lookup
+  uint32_t pf_dfa;         // value DFA of :method/:path/:authority whose candidate
+                           // entry is fetched right after its walk (most keyed rules), or kNone
+  uint32_t pad[3];         // header = 36 words
 };
 // Header-name table (LDS image): exact lower-case header names of the rules
 // -> field id, open addressing on the program.h name hash; slot =
 // {hash (0 = empty), len, field, image word offset of the zero-padded name}.
 // Replaces the walk of the header-name DFA when it fits kMaxNameTabBytes.
 constexpr uint32_t kMaxNameTabBytes = 8192;
-static_assert(sizeof(HttpHeader) == 128, "header is 32 words");
+static_assert(sizeof(HttpHeader) == 144, "header is 36 words");
 
 // ---------------------------------------------------------------- Kafka --
 // Rule semantics follow pkg/kafka/policy.go:144-225 and

@@ -60,6 +60,9 @@ EXPORTED_SYMBOLS = (
     "l7m_http_record_size", "l7m_pack_http", "l7m_eval", "l7m_eval_device",
     "l7m_alloc_pinned", "l7m_free_pinned", "l7m_abi_version", "l7m_device_count",
     "l7m_compile_http_policies", "l7m_ruleset_policy_index", "l7m_ruleset_rule_origin",
+    "l7m_batcher_create", "l7m_batcher_set_ruleset", "l7m_batcher_eval", "l7m_batcher_eval_http",
+    "l7m_batcher_stats", "l7m_batcher_destroy", "l7m_http_deny_body", "l7m_kafka_deny_response",
+    "l7m_proxy_stats_add",
 )
 
 
@@ -125,6 +128,16 @@ class _NetworkPolicy(ctypes.Structure):
                 ("egress", ctypes.POINTER(_PortPolicy)), ("n_egress", ctypes.c_size_t)]
 
 
+class _BatcherOpts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("max_batch", ctypes.c_uint32),
+                ("max_delay_us", ctypes.c_uint32), ("device", ctypes.c_int32)]
+
+
+class _ProxyStats(ctypes.Structure):
+    _fields_ = [("received", ctypes.c_uint64), ("forwarded", ctypes.c_uint64), ("denied", ctypes.c_uint64),
+                ("error", ctypes.c_uint64)]
+
+
 class _RuleOrigin(ctypes.Structure):
     _fields_ = [("policy", ctypes.c_uint32), ("ingress", ctypes.c_uint32), ("port", ctypes.c_uint32),
                 ("port_rule", ctypes.c_uint32), ("http_rule", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
@@ -144,6 +157,22 @@ def _load() -> ctypes.CDLL:
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C cilium_amd/csrc` "
                           "(there is no CPU fallback)")
     lib = ctypes.CDLL(LIB_PATH)
+    if os.environ.get("L7M_LIB"):
+        # an experimental build (tools/build_variant.sh, an older round's
+        # library for A/B timing) may lack newer entry points: bind what exists
+        class _Tolerant:
+            def __init__(self, lib):
+                self.__dict__["_lib"] = lib
+
+            def __getattr__(self, name):
+                try:
+                    return getattr(self._lib, name)
+                except AttributeError:
+                    return ctypes.CFUNCTYPE(None)()
+
+            def __setattr__(self, name, value):
+                setattr(self._lib, name, value)
+        lib = _Tolerant(lib)
     P = ctypes.c_void_p
     sz = ctypes.c_size_t
     lib.l7m_compile_http.argtypes = [ctypes.POINTER(_HttpRule), sz, ctypes.POINTER(_Opts),
@@ -153,6 +182,17 @@ def _load() -> ctypes.CDLL:
     lib.l7m_compile_http_policies.argtypes = [ctypes.POINTER(_NetworkPolicy), sz, ctypes.POINTER(_Opts),
                                               ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.l7m_ruleset_policy_index.argtypes = [P, ctypes.c_char_p]
+    lib.l7m_batcher_create.argtypes = [P, ctypes.POINTER(_BatcherOpts), ctypes.POINTER(P)]
+    lib.l7m_batcher_set_ruleset.argtypes = [P, P]
+    lib.l7m_batcher_eval.argtypes = [P, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int32)]
+    lib.l7m_batcher_eval_http.argtypes = [P, ctypes.POINTER(_HttpReq), ctypes.POINTER(ctypes.c_int32)]
+    lib.l7m_batcher_stats.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.l7m_batcher_destroy.argtypes = [P]
+    lib.l7m_batcher_destroy.restype = None
+    lib.l7m_http_deny_body.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
+    lib.l7m_http_deny_body.restype = sz
+    lib.l7m_kafka_deny_response.argtypes = [ctypes.c_char_p, sz, P, sz, ctypes.POINTER(sz)]
+    lib.l7m_proxy_stats_add.argtypes = [P, sz, ctypes.POINTER(_ProxyStats)]
     lib.l7m_ruleset_rule_origin.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(_RuleOrigin)]
     lib.l7m_release.argtypes = [P]
     lib.l7m_release.restype = None
@@ -524,6 +564,73 @@ class NetworkPolicyMap:
     def Allowed(self, reqs: Sequence[HTTPRequest], policy_names: Optional[Sequence[str]] = None) -> np.ndarray:
         v = self.verdicts(reqs, policy_names)
         return (v >= 0)
+
+
+class Batcher:
+    """l7m_batcher: blocking per-request verdicts shared in GPU batches (the
+    canAccess / decodeHeaders call shape, see include/l7match.h)."""
+
+    def __init__(self, ruleset: "RuleSet", max_batch: int = 0, max_delay_us: int = 0, device: int = 0):
+        self.ruleset = ruleset
+        opts = _BatcherOpts(ctypes.sizeof(_BatcherOpts), max_batch, max_delay_us, device)
+        h = ctypes.c_void_p()
+        rc = _lib.l7m_batcher_create(ruleset.handle, ctypes.byref(opts), ctypes.byref(h))
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_batcher_create failed")
+        self._h = h
+
+    def set_ruleset(self, ruleset: "RuleSet") -> None:
+        self.ruleset = ruleset
+        _lib.l7m_batcher_set_ruleset(self._h, ruleset.handle)
+
+    def eval(self, record: bytes) -> int:
+        v = ctypes.c_int32()
+        rc = _lib.l7m_batcher_eval(self._h, record, len(record), ctypes.byref(v))
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_batcher_eval failed")
+        return v.value
+
+    def stats(self) -> Tuple[int, int]:
+        b, r = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.l7m_batcher_stats(self._h, ctypes.byref(b), ctypes.byref(r))
+        return b.value, r.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.l7m_batcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def http_deny_body(configured: str = "") -> bytes:
+    """The 403 body AccessFilter sends on deny (envoy/cilium_l7policy.cc:89-95)."""
+    n = _lib.l7m_http_deny_body(_b(configured) or None, None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    _lib.l7m_http_deny_body(_b(configured) or None, buf, n + 1)
+    return buf.raw[:n]
+
+
+def kafka_deny_response(request: bytes) -> bytes:
+    """CreateResponse(ErrTopicAuthorizationFailed) bytes for a denied request."""
+    need = ctypes.c_size_t(0)
+    rc = _lib.l7m_kafka_deny_response(request, len(request), None, 0, ctypes.byref(need))
+    if rc not in (L7M_OK, L7M_ENOMEM):
+        raise L7Error(rc, "l7m_kafka_deny_response failed")
+    buf = ctypes.create_string_buffer(need.value)
+    rc = _lib.l7m_kafka_deny_response(request, len(request), buf, need.value, ctypes.byref(need))
+    if rc != L7M_OK:
+        raise L7Error(rc, "l7m_kafka_deny_response failed")
+    return buf.raw[:need.value]
+
+
+def proxy_stats(verdicts: np.ndarray) -> dict:
+    """Per-endpoint proxy counters of a batch of verdicts (l7m_proxy_stats_add)."""
+    v = np.ascontiguousarray(verdicts, dtype=np.int32)
+    st = _ProxyStats()
+    _lib.l7m_proxy_stats_add(v.ctypes.data, v.shape[0], ctypes.byref(st))
+    return {"received": st.received, "forwarded": st.forwarded, "denied": st.denied, "error": st.error}
 
 
 def matches_rule(records: Sequence[bytes], rules: Sequence[PortRuleKafka]) -> np.ndarray:

@@ -297,6 +297,54 @@ int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_byt
                     const void* d_rec_offsets, size_t n, void* d_verdicts, void* d_rule_hits,
                     void* hip_stream, uint32_t flags);
 
+/* ---- batching front-end (the call-site shape of the reference) ------------
+ * canAccess (pkg/proxy/kafka.go:116-152) and AccessFilter::decodeHeaders
+ * (envoy/cilium_l7policy.cc:126-186) decide one request per call on the
+ * connection's goroutine / worker thread.  l7m_batcher keeps that blocking
+ * per-request call: any number of threads call l7m_batcher_eval; their
+ * records share one l7m_eval, flushed when max_batch requests are pending or
+ * the first has waited max_delay_us, while the next batch fills.
+ * l7m_batcher_set_ruleset swaps the rules for later batches (the
+ * Redirect.updateRules policy update, pkg/proxy/redirect.go:68-74). */
+typedef struct l7m_batcher l7m_batcher;
+typedef struct {
+  uint32_t struct_size;  /* sizeof(l7m_batcher_opts); 0 = defaults          */
+  uint32_t max_batch;    /* requests per evaluation (0 = 65536)             */
+  uint32_t max_delay_us; /* longest wait of a batch's first request (0 = 200) */
+  int32_t device;        /* HIP device the batches run on                   */
+} l7m_batcher_opts;
+int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batcher** out);
+int l7m_batcher_set_ruleset(l7m_batcher* b, l7m_ruleset* rs);
+/* One request (a record as in the arena); blocks until its batch is decided. */
+int l7m_batcher_eval(l7m_batcher* b, const uint8_t* record, size_t len, int32_t* verdict);
+int l7m_batcher_eval_http(l7m_batcher* b, const l7m_http_request* req, int32_t* verdict);
+int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests);
+void l7m_batcher_destroy(l7m_batcher* b);
+
+/* ---- verdict side effects (host; for requests the GPU decided) ------------
+ * l7m_http_deny_body: the 403 body AccessFilter sends on deny: the configured
+ * denied_403_body, "Access denied" when empty, CRLF-terminated
+ * (envoy/cilium_l7policy.cc:89-95, 169-181).  Returns its length; writes up
+ * to cap-1 bytes + NUL.
+ * l7m_kafka_deny_response: the bytes handleRequest enqueues for a denied
+ * Kafka request, CreateResponse(ErrTopicAuthorizationFailed)
+ * (pkg/proxy/kafka.go:245-259, pkg/kafka/request.go:158-182,
+ * pkg/kafka/response.go) as optiopay's Resp.Bytes(version): every topic /
+ * partition of the request with error 29.  *out_len = the response size
+ * (L7M_ENOMEM when cap is smaller); L7M_EUNSUPPORTED for kinds ReadRequest
+ * leaves untyped ("unsupported request API key"); L7M_EINVAL if the request
+ * does not decode.
+ * l7m_proxy_stats_add: per-endpoint proxy counters of a batch
+ * (Endpoint.UpdateProxyStatistics, pkg/endpoint/endpoint.go:2099-2122):
+ * received, forwarded (allowed), denied, error (ReadRequest failed /
+ * unsupported). */
+typedef struct {
+  uint64_t received, forwarded, denied, error;
+} l7m_proxy_stats;
+size_t l7m_http_deny_body(const char* configured, char* out, size_t cap);
+int l7m_kafka_deny_response(const uint8_t* req, size_t len, uint8_t* out, size_t cap, size_t* out_len);
+int l7m_proxy_stats_add(const int32_t* verdicts, size_t n, l7m_proxy_stats* stats);
+
 /* Pinned host memory helpers (cgo may not retain Go pointers across calls). */
 int l7m_alloc_pinned(size_t bytes, void** out);
 void l7m_free_pinned(void* p);

@@ -276,3 +276,67 @@ def wrapper_set(value, codec, version=0, bad_crc=False):
         crc ^= 1
     m = struct.pack(">I", crc) + body
     return struct.pack(">qi", 0, len(m)) + m
+
+
+# ---- deny responses: CreateResponse(ErrTopicAuthorizationFailed) ----------
+# Test-side restatement of pkg/kafka/response.go + optiopay Resp.Bytes
+# (messages.go:595, 896, 1102, 1327, 1512, 1697, 1956), used to check
+# libl7match's l7m_kafka_deny_response.
+ERR_TOPIC_AUTHORIZATION_FAILED = 29
+ZERO_TIME_MILLIS = -6795364578871  # time.Time{}.UnixNano() (wrapped) / 1e6
+
+
+def deny_response(kind, version, correlation, topics):
+    """topics: [(name, [partition ids])] (names only for metadata)."""
+    e = ERR_TOPIC_AUTHORIZATION_FAILED
+    out = struct.pack(">i", correlation)
+    if kind == PRODUCE:
+        out += struct.pack(">i", len(topics))
+        for name, parts in topics:
+            out += s(name) + struct.pack(">i", len(parts))
+            for p in parts:
+                out += struct.pack(">ihq", p, e, 0) + (struct.pack(">q", 0) if version >= 2 else b"")
+        if version >= 1:
+            out += struct.pack(">i", 0)
+    elif kind == FETCH:
+        out += (struct.pack(">i", 0) if version >= 1 else b"") + struct.pack(">i", len(topics))
+        for name, parts in topics:
+            out += s(name) + struct.pack(">i", len(parts))
+            for p in parts:
+                out += struct.pack(">ihq", p, e, 0)
+                if version >= 4:
+                    out += struct.pack(">q", 0) + (struct.pack(">q", 0) if version >= 5 else b"") + struct.pack(">i", 0)
+                out += struct.pack(">i", 0)
+    elif kind == OFFSETS:
+        out += (struct.pack(">i", 0) if version >= 2 else b"") + struct.pack(">i", len(topics))
+        for name, parts in topics:
+            out += s(name) + struct.pack(">i", len(parts))
+            for p in parts:
+                out += struct.pack(">ih", p, e) + (struct.pack(">q", ZERO_TIME_MILLIS) if version >= 1 else b"")
+                out += struct.pack(">i", 0)
+    elif kind == METADATA:
+        out += (struct.pack(">i", 0) if version >= 3 else b"") + struct.pack(">i", 0)
+        out += (s("") if version >= 2 else b"") + (struct.pack(">i", 0) if version >= 1 else b"")
+        out += struct.pack(">i", len(topics))
+        for name in topics:
+            out += struct.pack(">h", e) + s(name) + (b"\x00" if version >= 1 else b"") + struct.pack(">i", 0)
+    elif kind == OFFSET_COMMIT:
+        out += (struct.pack(">i", 0) if version >= 3 else b"") + struct.pack(">i", len(topics))
+        for name, parts in topics:
+            out += s(name) + struct.pack(">i", len(parts))
+            for p in parts:
+                out += struct.pack(">ih", p, e)
+    elif kind == OFFSET_FETCH:
+        out += (struct.pack(">i", 0) if version >= 3 else b"") + struct.pack(">i", len(topics))
+        for name, parts in topics:
+            out += s(name) + struct.pack(">i", len(parts))
+            for p in parts:
+                out += struct.pack(">iq", p, 0) + s("") + struct.pack(">h", e)
+        if version >= 2:
+            out += struct.pack(">h", 0)
+    elif kind == CONSUMER_METADATA:
+        out += (struct.pack(">i", 0) if version >= 1 else b"") + struct.pack(">h", e)
+        out += (s("") if version >= 1 else b"") + struct.pack(">i", 0) + s("") + struct.pack(">i", 0)
+    else:
+        raise ValueError(kind)
+    return struct.pack(">i", len(out)) + out

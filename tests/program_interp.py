@@ -20,7 +20,7 @@ CR_REMOTE = 0x80000000
 HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_dfa off_dfas off_fields "
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
-              "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask").split()
+              "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi pf_dfa").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off").split()
 
@@ -47,7 +47,7 @@ class HttpProgram:
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
         h = self.h
         assert h["magic"] == 0x3448374C
-        assert len(HDR_FIELDS) == 30
+        assert len(HDR_FIELDS) == 33
         io = h["lds_image_off"]
         self.img = self.w[io:io + h["lds_image_words"]]
         self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
@@ -203,8 +203,12 @@ class HttpProgram:
                 eval_field(f, rec[pos:pos + ln])
             pos += ln
         if h["has_name_dfa"]:
+            lmask = h["name_len_hi"] << 32 | h["name_len_lo"]
             for e in dirs:
                 nl, vl = e & 0xFFFF, e >> 16
+                if not (lmask >> min(nl, 63)) & 1:  # no referenced name has this length
+                    pos += nl + vl
+                    continue
                 code = self.walk(h["n_dfas"], rec[pos:pos + nl])
                 if code & LATCHED:
                     f = 3 + (code & ~LATCHED)

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build an experimental libl7match variant: tools/build_variant.sh NAME "-DFLAG ..."
+# -> variants/NAME.so (same sources, extra compiler flags); bench.py / tests
+# load it with L7M_LIB=variants/NAME.so.
+set -eu
+cd "$(dirname "$0")/.."
+NAME=$1; FLAGS=${2:-}
+B=cilium_amd/csrc/build_$NAME
+mkdir -p $B variants
+for f in regex_ecma regex_re2 dfa_pack http_compile kafka_compile l7m_api l7m_side l7m_batch; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-result $FLAGS -D__HIP_PLATFORM_AMD__ \
+    -I/opt/rocm/include -x c++ -c cilium_amd/csrc/$f.cc -o $B/$f.o &
+done
+for f in l7m_kernels l7m_kafka; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-result $FLAGS --offload-arch=gfx950 \
+    -munsafe-fp-atomics -c cilium_amd/csrc/$f.hip -o $B/$f.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o variants/$NAME.so $B/*.o
+echo "built variants/$NAME.so"

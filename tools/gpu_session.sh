@@ -27,6 +27,8 @@ for s in "$@"; do
     prof:*) c=${s#prof:}; step prof_$c 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_$c -o run --output-format csv -- python3 -u bench.py --config $c --steps 20 --warmup 2 --no-cpu-baseline || exit $? ;;
     pmc:*) c=${s#pmc:}; cfg=${c%%:*}; ctr=${c#*:}
            step pmc_${cfg}_$ctr 300 rocprofv3 --pmc $ctr -d $PWD/$OUT/pmc_${cfg}_$ctr -o run --output-format csv -- python3 -u bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline || exit $? ;;
+    var:*) v=${s#var:}; name=${v%%:*}; cfg=${v#*:}
+           L7M_LIB=variants/$name.so step var_${name}_$cfg 300 python -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
