@@ -82,12 +82,12 @@ int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
 }
 
 // ---- Kafka compressed-message second pass: per-device scratch ------------
-// The first pass queues gzip / snappy values; kafka_codec_kernel decodes them
-// in per-worker slabs.  Queues come from a small ring per device (a launch
+// The first pass queues the requests holding gzip / snappy messages;
+// kafka_codec_kernel re-reads them with the values decoded in per-worker slabs.  Queues come from a small ring per device (a launch
 // waits, on its stream, for the previous user of its queue); the slabs are
 // one pool per device, so second passes of concurrent launches are chained
 // through an event.  Without the scratch (allocation failure) the queue
-// capacity is 0 and compressed values report L7M_VERDICT_UNSUPPORTED.
+// capacity is 0 and such requests report L7M_VERDICT_UNSUPPORTED.
 constexpr int kCodecSlots = 8;
 constexpr uint32_t kCodecQueueCap = 1u << 20;
 
@@ -99,7 +99,7 @@ struct KafkaCodecDev {
   uint64_t slab_bytes = 0;
   hipEvent_t p2_done = nullptr;
   struct Slot {
-    KafkaCodecItem* items = nullptr;
+    uint32_t* recs = nullptr;
     uint32_t* qhdr = nullptr;
     uint32_t cap = 0;
     hipEvent_t done = nullptr;
@@ -154,7 +154,7 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
         return hipErrorOutOfMemory;
       }
       if (g.workers &&
-          hipMalloc(reinterpret_cast<void**>(&slot->items), kCodecQueueCap * sizeof(KafkaCodecItem)) == hipSuccess)
+          hipMalloc(reinterpret_cast<void**>(&slot->recs), kCodecQueueCap * sizeof(uint32_t)) == hipSuccess)
         slot->cap = kCodecQueueCap;
     }
     hipError_t e = hipStreamWaitEvent(stream, slot->done, 0);
@@ -163,7 +163,7 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
       slot->busy = false;
       return e;
     }
-    cq.items = slot->items;
+    cq.recs = slot->recs;
     cq.qhdr = slot->qhdr;
     cq.cap = g.workers ? slot->cap : 0;
     cq.workers = g.workers;
@@ -174,7 +174,7 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
   std::lock_guard<std::mutex> lk(g.mu);
   if (e == hipSuccess && n && !(flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) && cq.cap) {
     e = hipStreamWaitEvent(stream, g.p2_done, 0);
-    if (e == hipSuccess) e = launch_kafka_codec(dprog, arena, verdicts, hits, stream, cq);
+    if (e == hipSuccess) e = launch_kafka_codec(dprog, arena, arena_bytes, offs, n, verdicts, hits, stream, cq);
     if (e == hipSuccess) e = hipEventRecord(g.p2_done, stream);
   }
   const hipError_t e2 = hipEventRecord(slot->done, stream);

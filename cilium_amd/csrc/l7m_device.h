@@ -38,12 +38,13 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
                        unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags);
 
 // Device scratch of the Kafka path's compressed-message second pass: the
-// queue the first pass fills (header [0] pushed, [1] work counter, zeroed
-// before each launch) and `workers` slabs of slab_bytes for decoded sets.
+// queue of request indices the first pass fills (header [0] pushed, [1] work
+// counter, zeroed before each launch) and `workers` slabs of slab_bytes for
+// decoded sets.
 struct KafkaCodecQueue {
-  KafkaCodecItem* items = nullptr;
+  uint32_t* recs = nullptr;
   uint32_t* qhdr = nullptr;
-  uint32_t cap = 0;      // 0: every compressed value reports -3
+  uint32_t cap = 0;      // 0: every request with a compressed message reports -3
   uint32_t workers = 0;
   uint8_t* slabs = nullptr;
   uint64_t slab_bytes = 0;
@@ -53,7 +54,8 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
                         uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                         unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags,
                         const KafkaCodecQueue& cq);
-hipError_t launch_kafka_codec(const uint32_t* dprog, const uint8_t* arena, int32_t* verdicts,
-                              unsigned long long* hits, hipStream_t stream, const KafkaCodecQueue& cq);
+hipError_t launch_kafka_codec(const uint32_t* dprog, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
+                              uint64_t n, int32_t* verdicts, unsigned long long* hits, hipStream_t stream,
+                              const KafkaCodecQueue& cq);
 
 }  // namespace l7m

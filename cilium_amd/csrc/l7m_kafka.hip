@@ -115,19 +115,11 @@ __device__ __forceinline__ void rd_skip_bytes(Rd& d) {
 
 enum { kMsOk = 0, kMsErr = 1 };
 
-// Where the first pass queues compressed values for kafka_codec_kernel.
-struct KPush {
-  KafkaCodecItem* items;
-  uint32_t* qhdr;        // [0] items pushed (may exceed cap), [1] second-pass work counter
-  uint32_t cap;
-  const uint8_t* rec;    // record start in the memory the decoder reads (LDS stage or HBM)
-  uint64_t rec_off;      // record start in the arena
-  uint32_t rec_idx;
-  bool overflow;         // a value did not fit the queue: verdict -3
-};
-
 // readMessageSet (messages.go:357-483) over the next `size` bytes of d.
-__device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint32_t* crc_tab, KPush& q) {
+// A gzip / snappy message sets `comp`: its value is decoded, and the request
+// re-read, by the second pass (kafka_codec_kernel); a nil value cannot be
+// decompressed (gzip.NewReader / snappy.Decode fail).
+__device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint32_t* crc_tab, bool& comp) {
   if (size < 0 || size > kKafkaMaxParseBuf) return kMsErr;
   const uint32_t avail = d.len - d.pos;
   Rd r{d.p + d.pos, avail < static_cast<uint32_t>(size) ? avail : static_cast<uint32_t>(size), 0, false};
@@ -156,41 +148,16 @@ __device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint
     rd_i8(m);                              // magic
     const int8_t attr = rd_i8(m);
     if (version >= 1) rd_be(m, 8);         // timestamp
-    const int comp = attr & 3;
-    if (comp == 3) break;                  // `return nil, err` with err == nil
+    const int cm = attr & 3;
+    if (cm == 3) break;                    // `return nil, err` with err == nil
     rd_skip_bytes(m);                      // key
-    if (comp == 0) {
-      rd_skip_bytes(m);  // value
-      if (m.err) {
-        rc = kMsErr;
-        break;
-      }
-      continue;
-    }
-    // gzip / snappy: the value (DecodeBytes) is decoded by the second pass;
-    // a nil value cannot be decompressed (gzip.NewReader / snappy.Decode fail)
-    const int32_t vn = rd_i32(m);
-    if (m.err || vn < 1 || vn > kKafkaMaxParseBuf || m.len - m.pos < static_cast<uint32_t>(vn)) {
+    const uint32_t vp = m.pos;
+    rd_skip_bytes(m);                      // value
+    if (m.err || (cm != 0 && m.pos - vp == 4)) {
       rc = kMsErr;
       break;
     }
-#ifdef L7M_NO_CODEC_QUEUE  // A/B diagnostic build: no second pass, compressed = unsupported
-    q.overflow = true;
-    const uint32_t at = q.cap;
-#else
-    const uint32_t at = atomicAdd(q.qhdr, 1u);
-#endif
-    if (at < q.cap) {
-      KafkaCodecItem it;
-      it.rec = q.rec_idx;
-      it.len = static_cast<uint32_t>(vn);
-      it.meta = kc_item_meta(q.rec_off + static_cast<uint64_t>(mb + m.pos - q.rec), static_cast<uint32_t>(comp),
-                             version);
-      q.items[at] = it;
-    } else {
-      q.overflow = true;
-    }
-    m.pos += static_cast<uint32_t>(vn);
+    comp |= cm != 0;
   }
   d.pos += r.pos;
   return rc;
@@ -382,7 +349,7 @@ constexpr uint32_t kTopicQ = 4;
 template <bool kLds>
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
                                               uint64_t limit, const uint32_t* crc_tab, uint16_t* tq,
-                                              KPush& q PROF_PARAM) {
+                                              bool& comp PROF_PARAM) {
 #ifdef L7M_PROF
   if (kLds) g_prof_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -502,7 +469,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
           rd_skip(d, 4);  // partition
           const int32_t mss = rd_i32(d);
           if (d.err) break;
-          if (read_message_set(d, mss, version, crc_tab, q) == kMsErr) {
+          if (read_message_set(d, mss, version, crc_tab, comp) == kMsErr) {
             ok = false;
             break;
           }
@@ -516,7 +483,6 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     }
     if (kind == 3 && version >= 4) rd_skip(d, 1);
     if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
-    if (q.overflow) return L7M_VERDICT_UNSUPPORTED;
     if (kind == 10) {
       // ConsumerMetadataReq: GetTopics() is nil and ruleMatches -> true.
       first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, false, kNone);
@@ -592,7 +558,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
                                                              const uint64_t* __restrict__ offs, uint64_t n,
                                                              int32_t* __restrict__ verdicts,
                                                              unsigned long long* __restrict__ hits, uint32_t stage,
-                                                             KafkaCodecItem* __restrict__ citems, uint32_t* qhdr,
+                                                             uint32_t* __restrict__ crecs, uint32_t* qhdr,
                                                              uint32_t qcap) {
   extern __shared__ __align__(16) uint32_t ksmem[];
 #ifdef L7M_PROF
@@ -701,26 +667,28 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
     if (lane < t.take) {
-      bool done = false;
-      KPush q{citems, qhdr, qcap, nullptr, o, static_cast<uint32_t>(t.cur + lane), false};
+      bool done = false, comp = false;
       if (lane < t.k && onext - o >= 4) {
         const uint8_t* rec = stg + (o - t.base);
-        q.rec = rec;
         const uint32_t msize = (static_cast<uint32_t>(rec[0]) << 24) | (static_cast<uint32_t>(rec[1]) << 16) |
                                (static_cast<uint32_t>(rec[2]) << 8) | rec[3];
         if (kAblate == 1) {
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, q PROF_ARG);
+          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, comp PROF_ARG);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        q.rec = arena + o;
-        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, q PROF_ARG)
+        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, comp PROF_ARG)
                       : L7M_VERDICT_PARSE_ERROR;
+      }
+      if (comp && verdict != L7M_VERDICT_PARSE_ERROR) {  // queue the request for the second pass
+        const uint32_t at = atomicAdd(qhdr, 1u);
+        if (at < qcap) crecs[at] = static_cast<uint32_t>(t.cur + lane);
+        else verdict = L7M_VERDICT_UNSUPPORTED;
       }
       verdicts[t.cur + lane] = verdict;
     }
@@ -766,7 +734,7 @@ static hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint
       set_lds_attr_once(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate, kCliLds>), kKLdsBytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate, kCliLds>), grid, dim3(kKBlock), lds, stream, dprog, arena,
-                     arena_bytes, offs, n, verdicts, hits, stage, cq.items, cq.qhdr, cq.cap);
+                     arena_bytes, offs, n, verdicts, hits, stage, cq.recs, cq.qhdr, cq.cap);
   return hipGetLastError();
 }
 
@@ -812,15 +780,18 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
 
 namespace {
 
-// Second pass over the compressed values the first pass queued: one worker
-// per workgroup (lane 0; decoding is a serial bit stream), each with its own
-// slab for the decoded sets.  A value that fails turns its request's verdict
-// into -2 (ReadRequest error) once, moving its count from the verdict's
-// counter slot to slot 1; -3 when the slab or nesting limit was reached.
+// Second pass over the requests the first pass queued (ProduceReqs holding
+// gzip / snappy messages): one worker per workgroup (lane 0; decoding is a
+// serial bit stream), each with its own slab for decoded sets, re-reads the
+// request with every compressed value decoded (kc_check_produce).  A request
+// the reference's ReadRequest would fail becomes -2, moving its count from
+// the verdict's counter slot to slot 1; -3 where the slab or nesting limit
+// was reached.
 __global__ __launch_bounds__(64) void kafka_codec_kernel(const uint32_t* __restrict__ prog,
                                                          const uint8_t* __restrict__ arena,
-                                                         const KafkaCodecItem* __restrict__ items, uint32_t* qhdr,
-                                                         uint32_t qcap, int32_t* verdicts,
+                                                         const uint64_t* __restrict__ offs, uint64_t n_recs,
+                                                         uint64_t arena_bytes, const uint32_t* __restrict__ recs,
+                                                         uint32_t* qhdr, uint32_t qcap, int32_t* verdicts,
                                                          unsigned long long* hits, uint8_t* slabs,
                                                          uint64_t slab_bytes) {
   if (threadIdx.x != 0) return;
@@ -831,36 +802,34 @@ __global__ __launch_bounds__(64) void kafka_codec_kernel(const uint32_t* __restr
   const uint32_t n = pushed < qcap ? pushed : qcap;
   KcInflateScratch s;
   for (uint32_t i = atomicAdd(qhdr + 1, 1u); i < n; i = atomicAdd(qhdr + 1, 1u)) {
-    const KafkaCodecItem it = items[i];
-    const int rc = kc_check_value(arena + kc_item_offset(it.meta), it.len, kc_item_codec(it.meta),
-                                  kc_item_version(it.meta), slab, static_cast<uint32_t>(slab_bytes), crc_tab, s);
+    const uint32_t ri = recs[i];
+    if (ri >= n_recs) continue;
+    const uint64_t o = offs[ri];
+    // the first pass decoded this record in bounds: 4 + size bytes at o
+    const uint8_t* rec = arena + o;
+    const uint32_t len = 4u + ((static_cast<uint32_t>(rec[0]) << 24) | (static_cast<uint32_t>(rec[1]) << 16) |
+                               (static_cast<uint32_t>(rec[2]) << 8) | rec[3]);
+    if (o + len > arena_bytes) continue;
+    const int rc = kc_check_produce(rec, len, slab, static_cast<uint32_t>(slab_bytes), crc_tab, s);
     if (rc == kCodecOk) continue;
+    const int32_t v = verdicts[ri];  // this request's only writer after the first pass
     const int32_t nv = rc == kCodecErr ? L7M_VERDICT_PARSE_ERROR : L7M_VERDICT_UNSUPPORTED;
-    int32_t v = __hip_atomic_load(verdicts + it.rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      // an error anywhere fails the request whatever else could not be decoded
-      if (v == L7M_VERDICT_PARSE_ERROR || (v == L7M_VERDICT_UNSUPPORTED && nv == L7M_VERDICT_UNSUPPORTED)) break;
-      const int32_t prev = atomicCAS(verdicts + it.rec, v, nv);
-      if (prev == v) {
-        if (hits && v != L7M_VERDICT_UNSUPPORTED) {
-          const uint32_t slot = v >= 0 ? static_cast<uint32_t>(v) + 2u : 0u;
-          atomicAdd(hits + slot, ~0ull);  // -1
-          atomicAdd(hits + 1, 1ull);
-        }
-        break;
-      }
-      v = prev;
+    verdicts[ri] = nv;
+    if (hits) {
+      atomicAdd(hits + (v >= 0 ? static_cast<uint32_t>(v) + 2u : 0u), ~0ull);  // -1
+      atomicAdd(hits + 1, 1ull);  // -2 and -3 share slot 1
     }
   }
 }
 
 }  // namespace
 
-hipError_t launch_kafka_codec(const uint32_t* dprog, const uint8_t* arena, int32_t* verdicts,
-                              unsigned long long* hits, hipStream_t stream, const KafkaCodecQueue& cq) {
-  if (!cq.cap || !cq.workers) return hipSuccess;
-  hipLaunchKernelGGL(kafka_codec_kernel, dim3(cq.workers), dim3(64), 0, stream, dprog, arena, cq.items, cq.qhdr, cq.cap,
-                     verdicts, hits, cq.slabs, cq.slab_bytes);
+hipError_t launch_kafka_codec(const uint32_t* dprog, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
+                              uint64_t n, int32_t* verdicts, unsigned long long* hits, hipStream_t stream,
+                              const KafkaCodecQueue& cq) {
+  if (!cq.cap || !cq.workers || !n) return hipSuccess;
+  hipLaunchKernelGGL(kafka_codec_kernel, dim3(cq.workers), dim3(64), 0, stream, dprog, arena, offs, n, arena_bytes,
+                     cq.recs, cq.qhdr, cq.cap, verdicts, hits, cq.slabs, cq.slab_bytes);
   return hipGetLastError();
 }
 

@@ -437,26 +437,16 @@ struct KcFrame {
   uint32_t len, pos, slab_top;
 };
 
-// Decode one compressed value into slab[top, ...) and check the decoded set
-// (and every compressed set nested in it) as readMessageSet would.
-__host__ __device__ inline int kc_check_value(const uint8_t* val, uint32_t vlen, uint32_t codec, int16_t version,
-                                              uint8_t* slab, uint32_t slab_bytes, const uint32_t* crc_tab,
-                                              KcInflateScratch& s) {
-  KcFrame st[kCodecMaxDepth];
-  uint32_t sp = 0, top = 0;
+// readMessageSet over the sets on st[0, sp): each message is checked as the
+// reference's decoder would, and a compressed value is decoded into
+// slab[top, ...) (top: the first free slab byte) and its set pushed (at most `max_sp` frames).  Returns at the
+// first value that fails (kCodecErr) or could not be decoded here
+// (kCodecUnsupported: nesting or slab limit).
+__host__ __device__ inline int kc_walk(KcFrame* st, uint32_t sp, uint32_t max_sp, uint32_t top, int16_t version,
+                                       uint8_t* slab, uint32_t slab_bytes, const uint32_t* crc_tab,
+                                       KcInflateScratch& s) {
   const uint32_t max_out = static_cast<uint32_t>(kKafkaMaxParseBuf);
-  auto decode = [&](const uint8_t* src, uint32_t n, uint32_t cdc) -> int {
-    if (sp >= kCodecMaxDepth) return kCodecUnsupported;
-    uint32_t out = 0;
-    const uint32_t cap = slab_bytes - top;
-    const int rc = cdc == kCodecGzip ? kc_gunzip(src, n, slab + top, cap, max_out, &out, crc_tab, s)
-                                     : kc_unsnappy(src, n, slab + top, cap, max_out, &out);
-    if (rc != kCodecOk) return rc;
-    st[sp++] = KcFrame{slab + top, out, 0, top};
-    top += out;
-    return kCodecOk;
-  };
-  int rc = decode(val, vlen, codec);
+  int rc = kCodecOk;
   while (rc == kCodecOk && sp > 0) {
     KcFrame& f = st[sp - 1];
     KcRd r{f.p, f.len, f.pos, false};
@@ -468,11 +458,11 @@ __host__ __device__ inline int kc_check_value(const uint8_t* val, uint32_t vlen,
     } else if (msz > kKafkaMaxParseBuf) {
       rc = kCodecErr;  // allocParseBuf
     } else if (r.len - r.pos < static_cast<uint32_t>(msz)) {
-      pop = true;  // truncated last message is ignored
+      r.pos = r.len;  // truncated last message is ignored (and consumed)
+      pop = true;
     } else {
       const uint8_t* mb = r.p + r.pos;
       r.pos += static_cast<uint32_t>(msz);
-      f.pos = r.pos;
       KcRd m{mb, static_cast<uint32_t>(msz), 0, false};
       const uint32_t crc = static_cast<uint32_t>(kc_be(m, 4));
       if (msz <= 4) {
@@ -490,17 +480,102 @@ __host__ __device__ inline int kc_check_value(const uint8_t* val, uint32_t vlen,
         } else {
           kc_bytes(m, &ko, &kl);
           kc_bytes(m, &vo, &vl);
-          if (m.err) rc = kCodecErr;
-          else if (comp != 0) rc = decode(mb + vo, vl, comp);
+          if (m.err) {
+            rc = kCodecErr;
+          } else if (comp != 0) {
+            if (sp >= max_sp) {
+              rc = kCodecUnsupported;
+            } else {
+              uint32_t out = 0;
+              const uint32_t cap = slab_bytes - top;
+              rc = comp == kCodecGzip ? kc_gunzip(mb + vo, vl, slab + top, cap, max_out, &out, crc_tab, s)
+                                      : kc_unsnappy(mb + vo, vl, slab + top, cap, max_out, &out);
+              if (rc == kCodecOk) {
+                st[sp++] = KcFrame{slab + top, out, 0, top};
+                top += out;
+              }
+            }
+          }
         }
       }
     }
+    f.pos = r.pos;  // bytes of the set consumed so far (read by kc_check_produce)
     if (pop) {
       top = st[sp - 1].slab_top;
       --sp;
     }
   }
   return rc;
+}
+
+// Decode one compressed value into the slab and check the decoded set (and
+// every compressed set nested in it) as readMessageSet would.
+__host__ __device__ inline int kc_check_value(const uint8_t* val, uint32_t vlen, uint32_t codec, int16_t version,
+                                              uint8_t* slab, uint32_t slab_bytes, const uint32_t* crc_tab,
+                                              KcInflateScratch& s) {
+  KcFrame st[kCodecMaxDepth];
+  uint32_t out = 0;
+  const uint32_t max_out = static_cast<uint32_t>(kKafkaMaxParseBuf);
+  const int rc = codec == kCodecGzip ? kc_gunzip(val, vlen, slab, slab_bytes, max_out, &out, crc_tab, s)
+                                     : kc_unsnappy(val, vlen, slab, slab_bytes, max_out, &out);
+  if (rc != kCodecOk) return rc;
+  st[0] = KcFrame{slab, out, 0, 0};
+  return kc_walk(st, 1, kCodecMaxDepth, out, version, slab, slab_bytes, crc_tab, s);
+}
+
+// DecodeString (serialization.go:120-153), bytes skipped.
+__host__ __device__ inline void kc_skip_str(KcRd& d) {
+  const int16_t n = static_cast<int16_t>(kc_be(d, 2));
+  if (d.err || n < 1) return;
+  if (d.len - d.pos < static_cast<uint32_t>(n)) {
+    d.pos = d.len;
+    d.err = true;
+    return;
+  }
+  d.pos += static_cast<uint32_t>(n);
+}
+
+// Second-pass check of one ProduceReq record (4-byte size prefix included,
+// `len` bytes readable) whose first-pass decode succeeded and met a
+// compressed message: the request is walked again as ReadProduceReq
+// (messages.go:1572-1628) reads it, and every message set is re-read with
+// its compressed values decoded.  kCodecErr where the reference's
+// ReadRequest fails, kCodecUnsupported where a value could not be decoded
+// here (and no later value fails).
+__host__ __device__ inline int kc_check_produce(const uint8_t* rec, uint32_t len, uint8_t* slab, uint32_t slab_bytes,
+                                                const uint32_t* crc_tab, KcInflateScratch& s) {
+  KcRd d{rec, len, 4, false};
+  const int16_t kind = static_cast<int16_t>(kc_be(d, 2));
+  const int16_t version = static_cast<int16_t>(kc_be(d, 2));
+  kc_be(d, 4);  // correlation id
+  kc_skip_str(d);  // client id
+  if (d.err || kind != 0) return kCodecOk;
+  if (version >= 3) kc_skip_str(d);  // transactional id
+  kc_be(d, 6);                       // acks, timeout
+  const int32_t nt = static_cast<int32_t>(kc_be(d, 4));
+  int worst = kCodecOk;
+  for (int32_t t = 0; t < nt && !d.err; ++t) {
+    kc_skip_str(d);  // topic
+    const int32_t np = static_cast<int32_t>(kc_be(d, 4));
+    if (d.err || np < 0 || np > kKafkaMaxParseBuf) break;
+    for (int32_t p = 0; p < np && !d.err; ++p) {
+      kc_be(d, 4);  // partition
+      const int32_t mss = static_cast<int32_t>(kc_be(d, 4));
+      if (d.err || mss < 0 || mss > kKafkaMaxParseBuf) break;
+      const uint32_t avail = d.len - d.pos;
+      KcFrame st[kCodecMaxDepth + 1];
+      st[0] = KcFrame{d.p + d.pos, avail < static_cast<uint32_t>(mss) ? avail : static_cast<uint32_t>(mss), 0, 0};
+      const int rc = kc_walk(st, 1, kCodecMaxDepth + 1, 0, version, slab, slab_bytes, crc_tab, s);
+      if (rc == kCodecErr) return rc;
+      if (rc == kCodecUnsupported) {
+        worst = rc;  // skip this set: a later one may still fail the request
+        break;
+      }
+      d.pos += st[0].pos;  // the set's consumed bytes (a set stopped early leaves the rest)
+    }
+    if (worst != kCodecOk) break;
+  }
+  return worst;
 }
 
 }  // namespace l7m

@@ -276,21 +276,4 @@ constexpr uint64_t kTopicApiKeyMask =
 // optiopay/kafka maxParseBufSize (vendor/github.com/optiopay/kafka/proto/utils.go:9).
 constexpr int64_t kKafkaMaxParseBuf = 100LL * 65535;
 
-// A compressed (gzip / snappy) message value queued by the Kafka kernel's
-// first pass for the second pass (kafka_codec_kernel): request index, value
-// length, and arena offset (46 bits) | codec << 46 | (u16)version << 48.
-struct KafkaCodecItem {
-  uint32_t rec;
-  uint32_t len;
-  uint64_t meta;
-};
-static_assert(sizeof(KafkaCodecItem) == 16, "codec item is 16 bytes");
-__host__ __device__ inline uint64_t kc_item_meta(uint64_t off, uint32_t codec, int16_t version) {
-  return (off & ((1ull << 46) - 1)) | static_cast<uint64_t>(codec & 3u) << 46 |
-         static_cast<uint64_t>(static_cast<uint16_t>(version)) << 48;
-}
-__host__ __device__ inline uint64_t kc_item_offset(uint64_t m) { return m & ((1ull << 46) - 1); }
-__host__ __device__ inline uint32_t kc_item_codec(uint64_t m) { return static_cast<uint32_t>(m >> 46) & 3u; }
-__host__ __device__ inline int16_t kc_item_version(uint64_t m) { return static_cast<int16_t>(m >> 48); }
-
 }  // namespace l7m

@@ -143,3 +143,54 @@ def deep_nesting(levels):
     for _ in range(levels - 1):
         v = K.gzip_member(K.wrapper_set(v, K.GZIP, 1))
     return K.produce(1, "c", [("t", [(0, K.wrapper_set(v, K.GZIP, 1))])])
+
+
+def _corrupt(rng, v):
+    v = bytearray(v)
+    for _ in range(rng.randrange(1, 3)):
+        if rng.random() < 0.6 or len(v) < 2:
+            v[rng.randrange(len(v))] ^= 1 << rng.randrange(8)
+        else:
+            del v[rng.randrange(1, len(v)):]
+    return bytes(v)
+
+
+def random_produce_requests(rng, n, framing_stops=False):
+    """ProduceReqs of 1-3 topics x 1-3 partitions whose message sets mix plain
+    messages and gzip / snappy wrappers (about a third of the compressed
+    values corrupted).  framing_stops adds what ends a set early (a bad-CRC
+    message, attribute 3, a truncated last message): the reference then
+    reads the set's unread bytes as the next partition's fields, which the
+    second pass must follow byte for byte."""
+    values = [(K.GZIP, K.gzip_member(INNER)), (K.SNAPPY, K.snappy_block(INNER)),
+              (K.SNAPPY, K.snappy_java(INNER, chunk=50)), (K.GZIP, K.gzip_member(INNER, level=1))]
+    out = []
+    for i in range(n):
+        ver = rng.choice((0, 1, 2, 3))
+        topics = []
+        for t in range(rng.randrange(1, 4)):
+            parts = []
+            for p in range(rng.randrange(1, 4)):
+                pieces = []
+                for _ in range(rng.randrange(1, 4)):
+                    r = rng.random()
+                    if r < 0.35:
+                        pieces.append(K.message_set(["x" * rng.randrange(0, 40)] * rng.randrange(1, 3), version=ver))
+                    else:
+                        codec, v = rng.choice(values)
+                        if rng.random() < 0.33:
+                            v = _corrupt(rng, v)
+                        pieces.append(K.wrapper_set(v, codec, ver))
+                if framing_stops and rng.random() < 0.3:
+                    k = rng.randrange(3)
+                    if k == 0:
+                        stop = K.message_set(["stop"], version=ver, bad_crc_at=0)
+                    elif k == 1:
+                        stop = K.message_set(["stop"], version=ver, compression=3)
+                    else:
+                        stop = K.message_set(["truncated" * 4], version=ver)[:-5]
+                    pieces.insert(rng.randrange(len(pieces) + 1), stop)
+                parts.append((p, b"".join(pieces)))
+            topics.append(("t" if rng.random() < 0.8 else "u", parts))
+        out.append(K.produce(ver, "c", topics, txn=None))
+    return out

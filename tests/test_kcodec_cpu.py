@@ -22,6 +22,7 @@ SLAB = 2 * 100 * 65535 + 65536  # the product's slab (l7m_api.cc)
 def _kcodec():
     lib = ctypes.CDLL(os.path.join(ROOT, "tests", "cpp", "bin", "libkcodec.so"))
     lib.kc_host_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32]
+    lib.kc_host_check_produce.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
     return lib
 
 
@@ -91,3 +92,26 @@ def test_device_decoder_nesting_and_slab_limits():
     big = K.gzip_member(K.message_set(["x" * 300_000], version=1))
     assert lib.kc_host_check(big, len(big), K.GZIP, 1, 100_000) == 2
     assert lib.kc_host_check(big, len(big), K.GZIP, 1, SLAB) == 0
+
+
+def test_second_pass_request_walk_matches_oracle_on_cases():
+    """kc_check_produce (the GPU second pass per queued request) on every
+    request case: a ReadRequest error exactly where the oracle has -2."""
+    lib = _kcodec()
+    for name, rec, exp in C.request_cases():
+        rc = lib.kc_host_check_produce(rec, len(rec), SLAB)
+        assert rc in (0, 1) and (rc == 1) == (exp == -2), (name, rc, exp)
+
+
+def test_second_pass_request_walk_matches_oracle_on_random_requests():
+    """Multi-topic / multi-partition produce requests mixing plain and
+    compressed messages, a third of the compressed values corrupted: the
+    second pass re-walks every set and fails exactly the requests the
+    oracle fails (the first pass accepts all of them: framing is valid)."""
+    lib = _kcodec()
+    recs = C.random_produce_requests(random.Random(5), 1500)
+    exp = _oracle(recs)
+    got = [lib.kc_host_check_produce(r, len(r), SLAB) for r in recs]
+    mism = [(i, exp[i], got[i]) for i in range(len(recs)) if (got[i] == 1) != (exp[i] == -2) or got[i] == 2]
+    assert not mism, mism[:10]
+    assert 0 < sum(1 for e in exp if e == -2) < len(exp)

@@ -80,3 +80,13 @@ def test_nesting_limit_reports_unsupported(gpu):
     rs = L.RuleSet.compile_kafka([L.PortRuleKafka(Topic="t")])
     assert rs.eval(arena, offs).tolist() == [0, L.VERDICT_UNSUPPORTED]
     assert KafkaOracle([L.PortRuleKafka(Topic="t")]).eval(arena, offs).tolist() == [0, 0]
+
+
+def test_random_multi_partition_produce_requests_gpu(gpu):
+    """Produce requests of several topics / partitions mixing plain and
+    compressed messages, corrupt values and sets that end early (bad CRC,
+    attribute 3, truncated message: the rest of the set is read as the next
+    partition's fields): verdicts and counters bit-exact with the oracle."""
+    recs = C.random_produce_requests(random.Random(23), 3000, framing_stops=True)
+    v = _check([L.PortRuleKafka(Topic="t")], recs)
+    assert (v == 0).any() and (v == -1).any() and (v == -2).any()
