@@ -74,11 +74,31 @@ def cpu_baseline(cfg, rules, seconds, threads):
     t = time.perf_counter()
     orc.eval(a, o, threads=threads)
     dt = time.perf_counter() - t
+    # one core, on a prefix of the same sample sized to ~seconds/4
+    n1 = int(min(len(o), max(min(len(o), n0 // 4), rate / threads * seconds / 4)))
+    a1, o1 = sample(20_000_000, n1)
+    t = time.perf_counter()
+    orc.eval(a1, o1, threads=1)
+    dt1 = time.perf_counter() - t
     note = "" if cfg != 5 else (" with /f{i}/ tails <= 24 bytes (longer ones make std::regex backtrack for "
                                 "seconds per request)")
     return {"value": len(o) / dt, "unit": "verdicts/s", "cores": threads, "kind": "port",
+            "single_thread_value": len(o1) / dt1, "cpu_model": cpu_model(),
             "sample": f"{len(o)} requests of config {cfg} (from requests [20M, 20M+{n})){note}, {dt:.1f} s, "
-                      f"oracle/l7oracle.cc (std::regex_match linear rule scan) on {threads} threads"}
+                      f"oracle/l7oracle.cc (std::regex_match linear rule scan) on {threads} threads; "
+                      f"single_thread_value: the first {len(o1)} of them on 1 thread, {dt1:.1f} s"}
+
+
+def cpu_model():
+    """The host CPU's model name (what `lscpu` prints), from /proc/cpuinfo."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def measured_traffic(cfg):
@@ -336,8 +356,17 @@ def run_mixed(args, world, rank, dev):
             dt = time.perf_counter() - t1
             n_tot, t_tot = n_tot + n, t_tot + dt
             samples.append(f"{n} requests of part config {p['gcfg']} in {dt:.1f} s")
+        # one core, on the first tenth of the last part's sample
+        n1 = max(1, len(o) // 10)
+        a1, o1 = W.requests(p["gcfg"], 20_000_000, n1, seed=p["seed"], n_rules=len(p["rules"]), threads=threads)
+        t1 = time.perf_counter()
+        orc.eval(a1, o1, threads=1)
+        st_rate = n1 / (time.perf_counter() - t1)
         res["cpu_baseline"] = {"value": n_tot / t_tot, "unit": "verdicts/s", "cores": threads, "kind": "port",
-                               "sample": "; ".join(samples) + f" (oracle/l7oracle.cc on {threads} threads)"}
+                               "single_thread_value": st_rate, "cpu_model": cpu_model(),
+                               "sample": "; ".join(samples) + f" (oracle/l7oracle.cc on {threads} threads); "
+                                         f"single_thread_value: {n1} requests of part config {p['gcfg']} on 1 "
+                                         f"thread"}
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -590,18 +590,6 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   h.zero_list = zero_span;
   h.single_entry = plan.single ? 1u : 0u;
   {
-    // the pseudo-header DFA most rules are keyed on: its candidate entry is
-    // fetched as soon as its walk ends, hiding the L2 latency behind the rest
-    h.pf_dfa = kNone;
-    size_t most = 0;
-    for (uint32_t f = 0; f < 3 && f < nf; ++f)
-      for (uint32_t g = 0; g < groups[f].size(); ++g) {
-        size_t k = 0;
-        for (const auto& kl : keyed[dfa_first[f] + g]) k += kl.size();
-        if (k > most) most = k, h.pf_dfa = dfa_first[f] + g;
-      }
-  }
-  {
     uint64_t m = 0;
     for (uint32_t f = 3; f < nf; ++f) m |= 1ull << std::min<size_t>(field_names[f].size(), 63);
     h.name_len_lo = static_cast<uint32_t>(m);
@@ -657,7 +645,12 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     }
     if (!ce.empty()) std::memcpy(P + dd[k].ct_off, ce.data(), ce.size() * sizeof(CandEntry));
     if (dd[k].lds_table != kNone) {
-      std::memcpy(I + dd[k].lds_table, d.table.data(), d.n_slots * 4ull);
+      // the LDS copy names rows by image word index (program.h kLdsRowShift)
+      const uint32_t t0 = dd[k].lds_table;
+      for (uint32_t s = 0; s < d.n_slots; ++s) {
+        const uint32_t e = d.table[s], next = e >> 8;
+        I[t0 + s] = next ? ((t0 + next) << kLdsRowShift) | (e & 0xffu) : (t0 << kLdsRowShift);
+      }
       for (uint32_t s = 0; dd[k].lds_es != kNone && s < d.n_slots; ++s)
         I16[dd[k].lds_es + s] = d.es[s] == kLatchedAccept ? static_cast<uint16_t>(kEs16Latched)
                                                            : static_cast<uint16_t>(d.es[s]);

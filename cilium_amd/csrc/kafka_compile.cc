@@ -163,6 +163,14 @@ bool key_ok(const KRule& r, uint32_t k) {  // CheckAPIKeyRole for table index k
 }  // namespace
 
 CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts& opts) {
+  const l7m_kafka_selector_rules all{rules, n, 1u, 0u};
+  return compile_kafka_map(&all, 1, nullptr, 0, opts);
+}
+
+// The rules of every L7DataMap entry, flattened entry by entry (verdict index
+// order); rule i applies to a source whose selector mask has bit group[i].
+CompileResult compile_kafka_map(const l7m_kafka_selector_rules* map, size_t n_entries,
+                                const l7m_identity_selectors* ids, size_t n_ids, const l7m_opts& opts) {
   (void)opts;
   CompileResult res;
   auto fail = [&](int st, const std::string& m) {
@@ -170,15 +178,30 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
     res.err = m;
     return res;
   };
-  if (n > 0 && !rules) return fail(L7M_EINVAL, "rules == NULL");
+  if (n_entries > 0 && !map) return fail(L7M_EINVAL, "map == NULL");
+  if (n_ids > 0 && !ids) return fail(L7M_EINVAL, "identities == NULL");
+  if (n_entries > kMaxKafkaGroups)
+    return fail(L7M_ETOOBIG, std::to_string(n_entries) + " L7DataMap entries > " + std::to_string(kMaxKafkaGroups));
+  uint64_t wild = 0;
+  bool selective = false;
+  size_t n = 0;
+  for (size_t g = 0; g < n_entries; ++g) {
+    if (map[g].n_rules > 0 && !map[g].rules) return fail(L7M_EINVAL, "entry " + std::to_string(g) + ": rules == NULL");
+    n += map[g].n_rules;
+    if (map[g].wildcard) wild |= 1ull << g;
+    else selective = true;
+  }
   if (n >= (1u << 30)) return fail(L7M_ETOOBIG, "too many rules");
 
   std::vector<KRule> kr(n);
-  for (size_t i = 0; i < n; ++i) {
-    std::string err;
-    int rc = sanitize(rules[i], &kr[i], &err);
-    if (rc != L7M_OK) return fail(rc, "rule " + std::to_string(i) + ": " + err);
-  }
+  std::vector<uint32_t> group(n);
+  for (size_t g = 0, i = 0; g < n_entries; ++g)
+    for (size_t j = 0; j < map[g].n_rules; ++j, ++i) {
+      std::string err;
+      int rc = sanitize(map[g].rules[j], &kr[i], &err);
+      if (rc != L7M_OK) return fail(rc, "rule " + std::to_string(i) + ": " + err);
+      group[i] = static_cast<uint32_t>(g);
+    }
 
   // string area: client ids and distinct topics
   std::string strings;
@@ -195,6 +218,7 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
     KafkaRuleDesc& d = desc[i];
     std::memset(&d, 0, sizeof d);
     d.client_idx = kNone;
+    d.group = group[i];
     if (r.keys.empty()) d.flags |= kKRuleAnyKey;
     for (int k : r.keys) {
       if (k < 32) d.keys_lo |= 1u << k;
@@ -271,7 +295,7 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
               ((d.flags & kKRuleVersion) ? kSlotVersionCond : 0u) | ((d.flags & kKRuleClient) ? kSlotClientCond : 0u) |
               (static_cast<uint32_t>(static_cast<uint16_t>(d.version)) << 16);
     sl.r0 = kv.second[0] | (kv.second.size() > 1 ? kSlotMore : 0u);
-    sl.r0_client = d.client_idx;
+    sl.r0_client = (d.client_idx == kNone ? 0xffffu : d.client_idx) | (d.group << 16);
     put_prefix(sl.pfx, kTopicInline, kv.first);
     ext[at].str_off = put_str(kv.first);
     ext[at].rules = push_list(kv.second);
@@ -284,6 +308,7 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
       if (k < 64 && ((kset_masks[s] >> k) & 1)) kind_ok[k] |= 1ull << s;
   }
 
+  if (client_ids.size() >= 0xffffu) return fail(L7M_ETOOBIG, "more than 65534 distinct ClientIDs");
   const uint32_t n_clients = table_size(client_ids.size());
   std::vector<KafkaClientSlot> cslots(n_clients);
   std::memset(cslots.data(), 0, cslots.size() * sizeof(KafkaClientSlot));
@@ -297,6 +322,35 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
     sl.str_len = static_cast<uint32_t>(kv.first.size());
     sl.idx = kv.second;
     put_prefix(sl.pfx, kClientInline, kv.first);
+  }
+
+  // source identity -> selector mask (only when some entry is not the wildcard)
+  const uint32_t n_id_slots = selective ? std::max<uint32_t>(2, table_size(n_ids)) : 0;
+  std::vector<KafkaIdSlot> id_slots(1 + n_id_slots);
+  std::memset(id_slots.data(), 0, id_slots.size() * sizeof(KafkaIdSlot));
+  id_slots[0].mask_lo = static_cast<uint32_t>(wild);
+  id_slots[0].mask_hi = static_cast<uint32_t>(wild >> 32);
+  for (size_t k = 0; k < n_ids && n_id_slots; ++k) {
+    const l7m_identity_selectors& e = ids[k];
+    if (e.identity == 0) return fail(L7M_EINVAL, "identity 0 is the unresolved source (no selector matches it)");
+    if (e.n_selectors > 0 && !e.selectors) return fail(L7M_EINVAL, "identity " + std::to_string(e.identity) +
+                                                                       ": selectors == NULL");
+    uint64_t m = wild;
+    for (size_t j = 0; j < e.n_selectors; ++j) {
+      if (e.selectors[j] >= n_entries)
+        return fail(L7M_EINVAL, "identity " + std::to_string(e.identity) + ": selector " +
+                                    std::to_string(e.selectors[j]) + " out of range");
+      m |= 1ull << e.selectors[j];
+    }
+    uint32_t at = kafka_id_hash(e.identity) & (n_id_slots - 1);
+    while (id_slots[1 + at].identity != 0) {
+      if (id_slots[1 + at].identity == e.identity)
+        return fail(L7M_EINVAL, "identity " + std::to_string(e.identity) + " listed twice");
+      at = (at + 1) & (n_id_slots - 1);
+    }
+    id_slots[1 + at].identity = e.identity;
+    id_slots[1 + at].mask_lo = static_cast<uint32_t>(m);
+    id_slots[1 + at].mask_hi = static_cast<uint32_t>(m >> 32);
   }
 
   uint32_t crc[256];
@@ -323,6 +377,8 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   h.off_pool = take(pool.size());
   h.off_crc = take(256);
   h.off_strings = take((strings.size() + 3) / 4);
+  h.off_ids = take(static_cast<uint64_t>(1 + n_id_slots) * sizeof(KafkaIdSlot) / 4);
+  h.n_id_slots = n_id_slots;
   if (w >= (1ull << 32)) return fail(L7M_ETOOBIG, "program exceeds 16 GiB");
   h.total_words = static_cast<uint32_t>(w);
 
@@ -337,6 +393,7 @@ CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opt
   if (!pool.empty()) std::memcpy(prog.data() + h.off_pool, pool.data(), pool.size() * 4);
   std::memcpy(prog.data() + h.off_crc, crc, sizeof crc);
   if (!strings.empty()) std::memcpy(prog.data() + h.off_strings, strings.data(), strings.size());
+  std::memcpy(prog.data() + h.off_ids, id_slots.data(), id_slots.size() * sizeof(KafkaIdSlot));
 
   res.program = std::move(prog);
   res.info.proto = L7M_PROTO_KAFKA;

@@ -118,7 +118,7 @@ uint32_t codec_workers() {
 
 hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                              const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
-                             hipStream_t stream, int cus, uint32_t flags) {
+                             hipStream_t stream, int cus, uint32_t flags, const uint32_t* ids) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   KafkaCodecDev& g = g_kcodec[dev];
@@ -170,7 +170,7 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
     cq.slabs = g.slabs;
     cq.slab_bytes = g.slab_bytes;
   }
-  hipError_t e = launch_kafka(dprog, h, arena, arena_bytes, offs, n, verdicts, hits, stream, cus, flags, cq);
+  hipError_t e = launch_kafka(dprog, h, arena, arena_bytes, offs, n, verdicts, hits, stream, cus, flags, cq, ids);
   std::lock_guard<std::mutex> lk(g.mu);
   if (e == hipSuccess && n && !(flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) && cq.cap) {
     e = hipStreamWaitEvent(stream, g.p2_done, 0);
@@ -185,7 +185,7 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
 }
 
 int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const void* offs, size_t n, void* verdicts,
-           void* hits, hipStream_t stream, uint32_t flags) {
+           void* hits, hipStream_t stream, uint32_t flags, const void* ids = nullptr) {
   auto* rs = const_cast<l7m_ruleset*>(crs);
   const uint32_t* dprog = nullptr;
   int cus = 0;
@@ -193,6 +193,7 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
   if (rc != L7M_OK) return rc;
   hipError_t e;
   if (rs->proto == L7M_PROTO_HTTP) {
+    if (ids) return L7M_EINVAL;  // HTTP records carry their remote identity
     HttpHeader h;
     std::memcpy(&h, rs->program.data(), sizeof h);
     if (http_stage_bytes(h) == 0) return L7M_ETOOBIG;
@@ -204,7 +205,8 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
     std::memcpy(&h, rs->program.data(), sizeof h);
     e = launch_kafka_both(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes,
                           static_cast<const uint64_t*>(offs), n, static_cast<int32_t*>(verdicts),
-                          static_cast<unsigned long long*>(hits), stream, cus, flags);
+                          static_cast<unsigned long long*>(hits), stream, cus, flags,
+                          static_cast<const uint32_t*>(ids));
   } else {
     return L7M_EINVAL;
   }
@@ -220,8 +222,8 @@ constexpr int kMaxDevices = 64;
 
 struct EvalCtx {
   hipStream_t stream = nullptr;
-  void *arena = nullptr, *offs = nullptr, *verd = nullptr, *hits = nullptr;
-  size_t cap_arena = 0, cap_offs = 0, cap_verd = 0, cap_hits = 0;
+  void *arena = nullptr, *offs = nullptr, *verd = nullptr, *hits = nullptr, *ids = nullptr;
+  size_t cap_arena = 0, cap_offs = 0, cap_verd = 0, cap_hits = 0, cap_ids = 0;
   std::vector<uint64_t> hhost;
   static int grow(void** p, size_t* cap, size_t want) {
     if (*cap >= want) return L7M_OK;
@@ -236,8 +238,9 @@ struct EvalCtx {
     *cap = sz;
     return L7M_OK;
   }
-  int reserve(size_t abytes, size_t n, size_t nctr) {
+  int reserve(size_t abytes, size_t n, size_t nctr, bool with_ids) {
     int rc = grow(&arena, &cap_arena, abytes);
+    if (rc == L7M_OK && with_ids) rc = grow(&ids, &cap_ids, n * 4);
     if (rc == L7M_OK) rc = grow(&offs, &cap_offs, n * 8);
     if (rc == L7M_OK) rc = grow(&verd, &cap_verd, n * 4);
     if (rc == L7M_OK) rc = grow(&hits, &cap_hits, nctr * 8);
@@ -303,6 +306,19 @@ int l7m_compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts* opt
   if (!out) return L7M_EINVAL;
   try {
     return finish_compile(compile_kafka(rules, n, norm_opts(opts)), L7M_PROTO_KAFKA, out, err, errlen);
+  } catch (const std::bad_alloc&) {
+    set_err(err, errlen, "out of host memory");
+    return L7M_ENOMEM;
+  }
+}
+
+int l7m_compile_kafka_map(const l7m_kafka_selector_rules* map, size_t n_entries,
+                          const l7m_identity_selectors* identities, size_t n_identities, const l7m_opts* opts,
+                          l7m_ruleset** out, char* err, size_t errlen) {
+  if (!out) return L7M_EINVAL;
+  try {
+    return finish_compile(compile_kafka_map(map, n_entries, identities, n_identities, norm_opts(opts)),
+                          L7M_PROTO_KAFKA, out, err, errlen);
   } catch (const std::bad_alloc&) {
     set_err(err, errlen, "out of host memory");
     return L7M_ENOMEM;
@@ -462,9 +478,25 @@ int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_byt
                 flags);
 }
 
+int l7m_eval_device_ids(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes, const void* d_offsets,
+                        size_t n, const void* d_ids, void* d_verdicts, void* d_hits, void* hip_stream,
+                        uint32_t flags) {
+  if (!rs || (n && (!d_arena || !d_offsets || !d_verdicts))) return L7M_EINVAL;
+  if (reinterpret_cast<uintptr_t>(d_arena) & 15) return L7M_EINVAL;
+  if (rs->proto != L7M_PROTO_KAFKA) return L7M_EINVAL;
+  return launch(rs, d_arena, arena_bytes, d_offsets, n, d_verdicts, d_hits, static_cast<hipStream_t>(hip_stream),
+                flags, d_ids);
+}
+
 int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
              const uint64_t* offsets, size_t n, int32_t* verdicts, uint64_t* hits, uint32_t flags) {
+  return l7m_eval_ids(rs, arena, arena_bytes, offsets, n, nullptr, verdicts, hits, flags);
+}
+
+int l7m_eval_ids(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes, const uint64_t* offsets,
+                 size_t n, const uint32_t* ids, int32_t* verdicts, uint64_t* hits, uint32_t flags) {
   if (!rs || (n && (!arena || !offsets || !verdicts))) return L7M_EINVAL;
+  if (ids && rs->proto != L7M_PROTO_KAFKA) return L7M_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return L7M_EDEVICE;
   if (n == 0) return L7M_OK;
@@ -475,15 +507,18 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
   const size_t abytes = (arena_bytes + 64) & ~size_t(3);
   EvalCtx* c = acquire_ctx(dev);
   if (!c) return L7M_EDEVICE;
-  int rc = c->reserve(abytes, n, nctr);
+  int rc = c->reserve(abytes, n, nctr, ids != nullptr);
   if (rc == L7M_OK) {
     const hipStream_t st = c->stream;
     bool ok = hipMemsetAsync(static_cast<uint8_t*>(c->arena) + arena_bytes, 0, abytes - arena_bytes, st) == hipSuccess &&
               hipMemcpyAsync(c->arena, arena, arena_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
               hipMemcpyAsync(c->offs, offsets, n * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+              (!ids || hipMemcpyAsync(c->ids, ids, n * 4, hipMemcpyHostToDevice, st) == hipSuccess) &&
               (!hits || hipMemsetAsync(c->hits, 0, nctr * 8, st) == hipSuccess);
     if (!ok) rc = L7M_EDEVICE;
-    if (rc == L7M_OK) rc = launch(rs, c->arena, arena_bytes, c->offs, n, c->verd, hits ? c->hits : nullptr, st, flags);
+    if (rc == L7M_OK)
+      rc = launch(rs, c->arena, arena_bytes, c->offs, n, c->verd, hits ? c->hits : nullptr, st, flags,
+                  ids ? c->ids : nullptr);
     if (rc == L7M_OK && hipMemcpyAsync(verdicts, c->verd, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = L7M_EDEVICE;
     if (rc == L7M_OK && hits && hipMemcpyAsync(c->hhost.data(), c->hits, nctr * 8, hipMemcpyDeviceToHost, st) != hipSuccess)

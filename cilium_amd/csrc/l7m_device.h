@@ -53,7 +53,7 @@ struct KafkaCodecQueue {
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena,
                         uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                         unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags,
-                        const KafkaCodecQueue& cq);
+                        const KafkaCodecQueue& cq, const uint32_t* ids);
 hipError_t launch_kafka_codec(const uint32_t* dprog, const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
                               uint64_t n, int32_t* verdicts, unsigned long long* hits, hipStream_t stream,
                               const KafkaCodecQueue& cq);

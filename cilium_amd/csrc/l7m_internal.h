@@ -68,6 +68,8 @@ std::string lower_ascii(const std::string& s);
 CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts& opts);
 CompileResult compile_http_policies(const l7m_network_policy* pols, size_t n, const l7m_opts& opts);
 CompileResult compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts& opts);
+CompileResult compile_kafka_map(const l7m_kafka_selector_rules* map, size_t n_entries,
+                                const l7m_identity_selectors* ids, size_t n_ids, const l7m_opts& opts);
 
 }  // namespace l7m
 

@@ -257,14 +257,16 @@ __device__ __forceinline__ bool key_ok(uint32_t flags, uint32_t keys_lo, uint32_
   return kind < 32 ? ((keys_lo >> kind) & 1u) : ((keys_hi >> (kind - 32)) & 1u);
 }
 
-// First rule of an ascending candidate list (ids < limit) passing rest_ok.
+// First rule of an ascending candidate list (ids < limit) that applies to
+// the source (gmask: its L7DataMap entries, GetRelevantRules) and passes
+// rest_ok.
 __device__ uint32_t first_in(const KView& v, Span s, uint32_t skip, uint32_t limit, int32_t kind, bool need_key,
-                             int16_t version, bool check_client, uint32_t client) {
+                             int16_t version, bool check_client, uint32_t client, uint64_t gmask) {
   for (uint32_t j = skip; j < s.len; ++j) {
     const uint32_t rid = v.pool[s.off + j];
     if (rid >= limit) break;
     const KafkaRuleDesc r = v.rules[rid];
-    if ((!need_key || key_ok(r.flags, r.keys_lo, r.keys_hi, kind)) &&
+    if (((gmask >> r.group) & 1ull) && (!need_key || key_ok(r.flags, r.keys_lo, r.keys_hi, kind)) &&
         rest_ok(r.flags, r.version, r.client_idx, version, check_client, client))
       return rid;
   }
@@ -290,14 +292,14 @@ __device__ __forceinline__ uint32_t intern_client(const KView& v, const uint8_t*
 // from the slot's own fields, later ones from the pool (kNone if none).
 // kok: the request kind's kind_ok bits.
 __device__ __forceinline__ uint32_t slot_first(const KView& v, const KafkaTopicSlot& sl, uint32_t at, uint64_t kok,
-                                               int32_t kind, int16_t version, uint32_t client) {
+                                               int32_t kind, int16_t version, uint32_t client, uint64_t gmask) {
   const uint32_t m = sl.meta;
-  if (((kok >> ((m >> 8) & 63u)) & 1ull) &&
+  if (((gmask >> (sl.r0_client >> 16)) & 1ull) && ((kok >> ((m >> 8) & 63u)) & 1ull) &&
       (!(m & kSlotVersionCond) || static_cast<int16_t>(m >> 16) == version) &&
-      (!(m & kSlotClientCond) || sl.r0_client == client))
+      (!(m & kSlotClientCond) || (sl.r0_client & 0xffffu) == (client & 0xffffu)))
     return sl.r0 & ~kSlotMore;
   if (!(sl.r0 & kSlotMore)) return kNone;
-  return first_in(v, v.ext[at].rules, 1, kNone, kind, true, version, true, client);
+  return first_in(v, v.ext[at].rules, 1, kNone, kind, true, version, true, client, gmask);
 }
 
 // Does slot `at` hold the name nm == t[0..tlen)?
@@ -311,10 +313,10 @@ __device__ __forceinline__ bool slot_is(const KView& v, const KafkaTopicSlot& sl
 // Probe from slot `at` (already fetched as sl) for the name nm.
 __device__ __forceinline__ uint32_t probe_topic(const KView& v, KafkaTopicSlot sl, uint32_t hash, const Name& nm,
                                                 const uint8_t* t, uint32_t tlen, uint64_t kok, int32_t kind,
-                                                int16_t version, uint32_t client) {
+                                                int16_t version, uint32_t client, uint64_t gmask) {
   for (uint32_t at = hash & (v.n_slots - 1);;) {
     if (sl.hash == 0) return kNone;
-    if (slot_is(v, sl, at, hash, nm, t, tlen)) return slot_first(v, sl, at, kok, kind, version, client);
+    if (slot_is(v, sl, at, hash, nm, t, tlen)) return slot_first(v, sl, at, kok, kind, version, client, gmask);
     at = (at + 1) & (v.n_slots - 1);
     sl = v.slots[at];
   }
@@ -325,10 +327,10 @@ __device__ __forceinline__ uint32_t probe_topic(const KView& v, KafkaTopicSlot s
 // reqTopicsMap coverage walk (policy.go:210-223).
 template <bool kLds>
 __device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t, uint32_t tlen, uint64_t kok,
-                                                int32_t kind, int16_t version, uint32_t client) {
+                                                int32_t kind, int16_t version, uint32_t client, uint64_t gmask) {
   if (!tlen || tlen > kMaxTopicLen || !v.n_slots) return kNone;
   const Name nm = load_name<kLds>(t, tlen);
-  return probe_topic(v, v.slots[nm.hash & (v.n_slots - 1)], nm.hash, nm, t, tlen, kok, kind, version, client);
+  return probe_topic(v, v.slots[nm.hash & (v.n_slots - 1)], nm.hash, nm, t, tlen, kok, kind, version, client, gmask);
 }
 
 // Topics are resolved after the decode, all lanes of the wave together
@@ -349,7 +351,7 @@ constexpr uint32_t kTopicQ = 4;
 template <bool kLds>
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
                                               uint64_t limit, const uint32_t* crc_tab, uint16_t* tq,
-                                              bool& comp PROF_PARAM) {
+                                              uint64_t gmask, bool& comp PROF_PARAM) {
 #ifdef L7M_PROF
   if (kLds) g_prof_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -370,7 +372,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     // request == nil: matchNonTopicRequests (policy.go:54-70), ClientID ignored.
     const bool topic_kind = kind >= 0 && kind < 64 && ((kTopicApiKeyMask >> kind) & 1ull);
     first = first_in(v, topic_kind ? spans[kidx] : spans[kKafkaKinds + kidx], 0, kNone, kind, false,
-                     version, false, kNone);
+                     version, false, kNone, gmask);
   } else {
     Rd d{rec, 4u + static_cast<uint32_t>(msize), 12, false};
     uint32_t coff, clen;
@@ -399,7 +401,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
         tq[64 * nq] = static_cast<uint16_t>(toff);
         ++nq;
       } else {
-        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid);
+        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid, gmask);
         maxf = f > maxf ? f : maxf;
       }
     };
@@ -485,9 +487,9 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
     if (kind == 10) {
       // ConsumerMetadataReq: GetTopics() is nil and ruleMatches -> true.
-      first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, false, kNone);
+      first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, false, kNone, gmask);
     } else if (ntop == 0) {
-      first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, true, cid);
+      first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, true, cid, gmask);
     } else {
 #ifdef L7M_PROF
       const uint64_t tr0 = __builtin_amdgcn_s_memtime();
@@ -496,10 +498,10 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       for (uint32_t r = 0; r < nq && maxf != kNone; ++r) {
         const uint32_t toff = tq[64 * r];
         const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
-        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid);
+        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid, gmask);
         maxf = f > maxf ? f : maxf;
       }
-      const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid);
+      const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid, gmask);
       first = j < maxf ? j : maxf;
 #ifdef L7M_PROF
       if (kLds) g_prof_rounds += __builtin_amdgcn_s_memtime() - tr0;
@@ -552,14 +554,16 @@ enum KHitMode { kKNoHits = 0, kKLdsHits = 1, kKGlobalHits = 2 };
 // its tile window is decoded from HBM.
 // kAblate (diagnostics only, L7M_FLAG_DIAG_*): 1 = stage records, no
 // decoding; 2 = decode without table lookups.
-template <int kHits, int kAblate, bool kCliLds>
+// kGroups: the program's rules belong to several L7DataMap entries, so each
+// request's source identity selects the rules that apply (else all do).
+template <int kHits, int kAblate, bool kCliLds, bool kGroups>
 __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
                                                              const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                              const uint64_t* __restrict__ offs, uint64_t n,
                                                              int32_t* __restrict__ verdicts,
                                                              unsigned long long* __restrict__ hits, uint32_t stage,
                                                              uint32_t* __restrict__ crecs, uint32_t* qhdr,
-                                                             uint32_t qcap) {
+                                                             uint32_t qcap, const uint32_t* __restrict__ ids) {
   extern __shared__ __align__(16) uint32_t ksmem[];
 #ifdef L7M_PROF
   uint64_t prof[5] = {0, 0, 0, 0, 0};
@@ -666,6 +670,22 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
 #ifdef L7M_PROF
     const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
+    // GetRelevantRules (pkg/policy/l4.go:110-129): the L7DataMap entries whose
+    // rules apply to this request's source identity
+    uint64_t gmask = ~0ull;
+    if (kGroups && lane < t.take) {
+      const KafkaIdSlot* it = reinterpret_cast<const KafkaIdSlot*>(prog + h.off_ids);
+      gmask = (static_cast<uint64_t>(it[0].mask_hi) << 32) | it[0].mask_lo;
+      const uint32_t id = ids ? ids[t.cur + lane] : 0u;
+      for (uint32_t at = kafka_id_hash(id) & (h.n_id_slots - 1); id; at = (at + 1) & (h.n_id_slots - 1)) {
+        const KafkaIdSlot e = it[1 + at];
+        if (e.identity == 0) break;  // not listed: the reference's nil identity
+        if (e.identity == id) {
+          gmask = (static_cast<uint64_t>(e.mask_hi) << 32) | e.mask_lo;
+          break;
+        }
+      }
+    }
     if (lane < t.take) {
       bool done = false, comp = false;
       if (lane < t.k && onext - o >= 4) {
@@ -676,13 +696,13 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, comp PROF_ARG);
+          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, gmask, comp PROF_ARG);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, comp PROF_ARG)
+        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, gmask, comp PROF_ARG)
                       : L7M_VERDICT_PARSE_ERROR;
       }
       if (comp && verdict != L7M_VERDICT_PARSE_ERROR) {  // queue the request for the second pass
@@ -726,15 +746,15 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   }
 }
 
-template <int kHits, int kAblate = 0, bool kCliLds = false>
+template <int kHits, int kAblate = 0, bool kCliLds = false, bool kGroups = false>
 static hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                            uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                           unsigned long long* hits, uint32_t stage, const KafkaCodecQueue& cq) {
+                           unsigned long long* hits, uint32_t stage, const KafkaCodecQueue& cq, const uint32_t* ids) {
   const hipError_t e =
-      set_lds_attr_once(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate, kCliLds>), kKLdsBytes);
+      set_lds_attr_once(reinterpret_cast<const void*>(kafka_eval_kernel<kHits, kAblate, kCliLds, kGroups>), kKLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate, kCliLds>), grid, dim3(kKBlock), lds, stream, dprog, arena,
-                     arena_bytes, offs, n, verdicts, hits, stage, cq.recs, cq.qhdr, cq.cap);
+  hipLaunchKernelGGL((kafka_eval_kernel<kHits, kAblate, kCliLds, kGroups>), grid, dim3(kKBlock), lds, stream, dprog, arena,
+                     arena_bytes, offs, n, verdicts, hits, stage, cq.recs, cq.qhdr, cq.cap, ids);
   return hipGetLastError();
 }
 
@@ -742,7 +762,8 @@ static hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint
 
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                         const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
-                        hipStream_t stream, int num_cus, uint32_t flags, const KafkaCodecQueue& cq) {
+                        hipStream_t stream, int num_cus, uint32_t flags, const KafkaCodecQueue& cq,
+                        const uint32_t* ids) {
   if (n == 0) return hipSuccess;
   const uint32_t n_ctr = h.n_rules + 2;
   const int mode = !hits ? kKNoHits : (n_ctr <= kKMaxLdsCounters ? kKLdsHits : kKGlobalHits);
@@ -762,19 +783,26 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const uint32_t st = static_cast<uint32_t>(stage);
   if (flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) {
     if (flags & L7M_FLAG_DIAG_COPY_ONLY)
-      return launch_k<kKNoHits, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq);
-    return launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq);
+      return launch_k<kKNoHits, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq, ids);
+    return launch_k<kKNoHits, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq, ids);
   }
-#define L7M_KAFKA_LAUNCH(M, C) \
-  return launch_k<M, 0, C>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq)
+#define L7M_KAFKA_LAUNCH(M, C, G) \
+  return launch_k<M, 0, C, G>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, st, cq, ids)
+#define L7M_KAFKA_LAUNCH_G(M, C)        \
+  {                                     \
+    if (groups) L7M_KAFKA_LAUNCH(M, C, true); \
+    L7M_KAFKA_LAUNCH(M, C, false);      \
+  }
+  const bool groups = h.n_id_slots != 0;
   if (cli_lds) {
-    if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, true);
-    if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, true);
-    L7M_KAFKA_LAUNCH(kKGlobalHits, true);
+    if (mode == kKNoHits) L7M_KAFKA_LAUNCH_G(kKNoHits, true);
+    if (mode == kKLdsHits) L7M_KAFKA_LAUNCH_G(kKLdsHits, true);
+    L7M_KAFKA_LAUNCH_G(kKGlobalHits, true);
   }
-  if (mode == kKNoHits) L7M_KAFKA_LAUNCH(kKNoHits, false);
-  if (mode == kKLdsHits) L7M_KAFKA_LAUNCH(kKLdsHits, false);
-  L7M_KAFKA_LAUNCH(kKGlobalHits, false);
+  if (mode == kKNoHits) L7M_KAFKA_LAUNCH_G(kKNoHits, false);
+  if (mode == kKLdsHits) L7M_KAFKA_LAUNCH_G(kKLdsHits, false);
+  L7M_KAFKA_LAUNCH_G(kKGlobalHits, false);
+#undef L7M_KAFKA_LAUNCH_G
 #undef L7M_KAFKA_LAUNCH
 }
 

@@ -67,14 +67,28 @@ __device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, c
 }
 
 // Walk `len` bytes at byte `pos` of the record through one packed DFA
-// (dfa_pack.h): per byte ONE dependent slot-table read,
-//     e = T[base + b];  base = (e & 0xff) == b ? e >> 8 : 0.
-// The dead state (base 0) is absorbing, so the exit test runs once per 4
-// bytes.  kLdsTab: tables in the LDS image, else in HBM.
-template <bool kLdsTab, class Src>
-__device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
-                                         const DfaDesc& dd, const Src& src, uint32_t pos, uint32_t len) {
-  const uint32_t* __restrict__ T = kLdsTab ? img + dd.lds_table : prog + dd.table_off;
+// (dfa_pack.h): per byte ONE dependent slot-table read.  The dead state is
+// absorbing, so the exit test runs once per 4 bytes.
+#define L7M_WALK_BYTES(STEP, DEAD)                                          \
+  {                                                                         \
+    for (; k + 4 <= len; k += 4) {                                          \
+      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);    \
+      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3); \
+      STEP(b0)                                                              \
+      STEP(b1)                                                              \
+      STEP(b2)                                                              \
+      STEP(b3)                                                              \
+      if (DEAD) break;                                                      \
+    }                                                                       \
+    if (!(DEAD))                                                            \
+      for (; k < len; ++k) STEP(src.byte(pos + k))                          \
+  }
+
+// HBM slot table: e = T[base + b]; base = (e & 0xff) == b ? e >> 8 : 0.
+template <class Src>
+__device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
+                                             const DfaDesc& dd, const Src& src, uint32_t pos, uint32_t len) {
+  const uint32_t* __restrict__ T = prog + dd.table_off;
   const uint32_t region = dd.region;
   uint32_t base = dd.start_base;
   uint32_t last = kNone;
@@ -87,22 +101,59 @@ __device__ __forceinline__ uint32_t walk(const uint32_t* __restrict__ img, const
     base = (e_ & 0xffu) == b_ ? (e_ >> 8) : 0u;            \
   }
   uint32_t k = 0;
-  if (base) {
-    for (; k + 4 <= len; k += 4) {
-      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
-      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
-      L7M_STEP(b0)
-      L7M_STEP(b1)
-      L7M_STEP(b2)
-      L7M_STEP(b3)
-      if (!base) break;
-    }
-    if (base)
-      for (; k < len; ++k) L7M_STEP(src.byte(pos + k))
-  }
+  if (base) L7M_WALK_BYTES(L7M_STEP, !base)
 #undef L7M_STEP
-  return end_code<kLdsTab>(img, prog, dd, base, last);
+  return end_code<false>(img, prog, dd, base, last);
 }
+
+// A walk through an LDS slot table, re-encoded by the compiler for it
+// (program.h kLdsRowShift): e = (image word index of the next row << 16) |
+// label, the dead row being the table's own row 0 (no label matches there).
+// A step is
+//     slot = (sel >> 16) + b;  e = img[slot];  sel = label(e) == b ? e : dead
+// with the word / byte selects folded into SDWA operands.  `slast` is the
+// slot of the last transition taken from a multi-pattern row (below lim).
+struct LdsChain {
+  uint32_t sel, dead, lim, slast;
+  __device__ __forceinline__ void init(const DfaDesc& dd) {
+    dead = dd.lds_table << kLdsRowShift;
+    lim = dd.lds_table + dd.region;
+    sel = (dd.lds_table + dd.start_base) << kLdsRowShift;
+    slast = kNone;
+  }
+  __device__ __forceinline__ void step(const uint32_t* __restrict__ img, uint32_t b) {
+    uint32_t s = (sel >> kLdsRowShift) + b;
+    asm("" : "+v"(s));  // one SDWA add, then the scale
+    const uint32_t e = img[s];
+    slast = (sel >> kLdsRowShift) < lim ? s : slast;
+    sel = (e & 0xffffu) == b ? e : dead;
+  }
+  __device__ __forceinline__ bool dead_now() const { return sel == dead; }
+  // continue the walk over bytes [k, len) of the field at pos
+  template <class Src>
+  __device__ __forceinline__ void run(const uint32_t* __restrict__ img, const Src& src, uint32_t pos, uint32_t len,
+                                      uint32_t k) {
+#define L7M_STEP(B) step(img, (B));
+    L7M_WALK_BYTES(L7M_STEP, dead_now())
+#undef L7M_STEP
+  }
+  __device__ __forceinline__ uint32_t code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
+                                           const DfaDesc& dd) const {
+    const uint32_t t0 = dead >> kLdsRowShift;
+    return end_code<true>(img, prog, dd, (sel >> kLdsRowShift) - t0, slast == kNone ? kNone : slast - t0);
+  }
+};
+
+template <class Src>
+__device__ __forceinline__ uint32_t walk_lds(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
+                                             const DfaDesc& dd, const Src& src, uint32_t pos, uint32_t len) {
+  LdsChain c;
+  c.init(dd);
+  if (dd.start_base) c.run(img, src, pos, len, 0);
+  return c.code(img, prog, dd);
+}
+
+#undef L7M_WALK_BYTES
 
 __device__ __forceinline__ bool set_has(const uint32_t* __restrict__ pool, Span s, uint32_t p) {
   for (uint32_t j = 0; j < s.len; ++j) {
@@ -178,8 +229,8 @@ struct Ctx {
 template <class Src>
 __device__ __forceinline__ uint32_t walk_dfa(const Ctx& c, uint32_t d, const Src& src, uint32_t pos, uint32_t len) {
   const DfaDesc& dd = c.dds[d];
-  if (dd.lds_table != kNone) return walk<true>(c.img, c.prog, dd, src, pos, len);
-  return walk<false>(c.img, c.prog, dd, src, pos, len);
+  if (dd.lds_table != kNone) return walk_lds(c.img, c.prog, dd, src, pos, len);
+  return walk_hbm(c.img, c.prog, dd, src, pos, len);
 }
 
 // Field id of the header name at byte `pos` (length len) of the record, via
@@ -327,28 +378,11 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   uint64_t present = 0;
   codes.clear(h.n_dfas);
   uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
-  // Candidate entry of the prefetch DFA (h.pf_dfa), loaded as soon as its
-  // walk ends so that the L2 latency overlaps the remaining walks.
-  u32x4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0}, pf2 = {0, 0, 0, 0};
-  auto prefetch = [&](uint32_t d, uint32_t code) {
-    if (!code) return;
-    const DfaDesc& dd = c.dds[d];
-    const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
-    const uint32_t mw = dd.lds_ctmask != kNone ? c.img[dd.lds_ctmask + (idx >> 5)] : c.prog[dd.ctmask_off + (idx >> 5)];
-    if (!((mw >> (idx & 31u)) & 1u)) return;
-    const u32x4* e = reinterpret_cast<const u32x4*>(dd.lds_ct != kNone ? c.img + dd.lds_ct + 16u * idx
-                                                                       : c.prog + dd.ct_off + 16u * idx);
-    pf0 = e[0];
-    pf1 = e[1];
-    pf2 = e[2];
-  };
   auto eval_field = [&](uint32_t f, uint32_t p, uint32_t len) {
     const FieldDesc& fd = c.fields[f];
     for (uint32_t k = 0; k < fd.ndfa; ++k) {
       const uint32_t d = fd.dfa_first + k;
-      const uint32_t code = walk_dfa(c, d, src, p, len);
-      codes.set(d, code);
-      if (d == h.pf_dfa) prefetch(d, code);
+      codes.set(d, walk_dfa(c, d, src, p, len));
     }
   };
   if (flags & L7M_HTTP_F_METHOD) {
@@ -461,10 +495,9 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     const u32x4* q = reinterpret_cast<const u32x4*>(e);
     check_entry(q[0], q[1], q[2]);
   };
-  if (h.pf_dfa != kNone && pf0.x) check_entry(pf0, pf1, pf2);
   for (uint32_t d = 0; d < h.n_dfas; ++d) {
     const uint32_t code = codes.get(d);
-    if (!code || d == h.pf_dfa) continue;
+    if (!code) continue;
     const DfaDesc& dd = c.dds[d];
     const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
     const uint32_t mw = dd.lds_ctmask != kNone ? c.img[dd.lds_ctmask + (idx >> 5)] : c.prog[dd.ctmask_off + (idx >> 5)];

@@ -85,6 +85,11 @@ struct CandEntry {
 static_assert(sizeof(CandEntry) == 64, "cand entry is 16 words");
 constexpr uint32_t kLatchedBit = 0x80000000u;
 constexpr uint32_t kEs16Latched = 0xffffu;
+// The LDS copy of a slot table names rows by image word index: entry =
+// (lds_table + next base) << kLdsRowShift | label, a dead transition (or
+// unowned slot) = lds_table << kLdsRowShift (the table's row 0, where no
+// label matches).  The image is < 64 Ki words (kLdsBytes), so indices fit.
+constexpr uint32_t kLdsRowShift = 16;
 
 // ---- HTTP kernel geometry and LDS budget -------------------------------
 // Shared by the compiler's LDS image sizing (http_compile.cc) and the kernel
@@ -159,9 +164,7 @@ struct HttpHeader {
   uint32_t ent_mask;       // its slot count - 1
   uint32_t name_len_lo;    // bit l (l < 64, 63 = longer) set iff a referenced header
   uint32_t name_len_hi;    // name has that length: other names skip the lookup
-  uint32_t pf_dfa;         // value DFA of :method/:path/:authority whose candidate
-                           // entry is fetched right after its walk (most keyed rules), or kNone
-  uint32_t pad[3];         // header = 36 words
+  uint32_t pad[4];         // header = 36 words
 };
 // Header-name table (LDS image): exact lower-case header names of the rules
 // -> field id, open addressing on the program.h name hash; slot =
@@ -179,7 +182,8 @@ struct KafkaRuleDesc {
   uint32_t keys_lo;     // apiKeyInt as a bitmask over kinds 0..63 (unless kKRuleAnyKey)
   uint32_t keys_hi;
   uint32_t client_idx;  // interned ClientID when kKRuleClient (KafkaClientSlot::idx)
-  uint32_t pad[3];
+  uint32_t group;       // L7DataMap entry (bit of the source's selector mask)
+  uint32_t pad[2];
 };
 constexpr uint32_t kKRuleAnyKey = 1u, kKRuleVersion = 2u, kKRuleTopic = 4u, kKRuleClient = 8u;
 
@@ -194,7 +198,7 @@ struct KafkaTopicSlot {
   uint32_t hash;
   uint32_t meta;       // len (8) | kset (6) << 8 | version-cond << 14 | client-cond << 15 | (u16)version << 16
   uint32_t r0;         // first rule id | (more than one rule) << 31
-  uint32_t r0_client;  // its client_idx
+  uint32_t r0_client;  // its client_idx (low 16 bits, 0xffff = none) | its group << 16
   uint32_t pfx[kTopicInline / 4];
 };
 struct KafkaTopicExt {
@@ -236,11 +240,29 @@ struct KafkaHeader {
   uint32_t n_clients;    // power of two (0 when no rule has a ClientID)
   uint32_t off_ext;      // KafkaTopicExt[n_slots]
   uint32_t off_kind_ok;  // u64[kKafkaKinds]
-  uint32_t pad[3];
+  uint32_t off_ids;      // KafkaIdSlot[1 + n_id_slots]: [0] = the wildcard entries' mask
+  uint32_t n_id_slots;   // power of two; 0 = one wildcard entry (every rule applies)
+  uint32_t pad;
   // Ascending ids of the rules whose CheckAPIKeyRole(kind) holds:
   Span notopic_by_kind[kKafkaKinds];  // ... and Topic == ""
   Span all_by_kind[kKafkaKinds];      // ... any Topic
 };
+// Source identity -> mask of the L7DataMap entries whose rules apply to it
+// (the selecting entries' bits | the wildcard entries' bits); open
+// addressing on kafka_id_hash, identity 0 = empty.
+struct KafkaIdSlot {
+  uint32_t identity;
+  uint32_t pad;
+  uint32_t mask_lo, mask_hi;
+};
+constexpr uint32_t kMaxKafkaGroups = 64;
+__host__ __device__ inline uint32_t kafka_id_hash(uint32_t id) {
+  id ^= id >> 16;
+  id *= 0x7feb352du;
+  id ^= id >> 15;
+  id *= 0x846ca68bu;
+  return id ^ (id >> 16);
+}
 static_assert(sizeof(KafkaRuleDesc) == 32, "rule desc is 8 words");
 static_assert(sizeof(KafkaTopicSlot) == 32, "topic slot is 8 words");
 static_assert(sizeof(KafkaTopicExt) == 16, "topic ext is 4 words");

@@ -4,8 +4,9 @@
 // ECMAScript scanner/compiler (GCC 11: bits/regex_scanner.tcc,
 // bits/regex_compiler.tcc) because that is the engine Envoy links for
 // HeaderMatcher regexes (reference: envoy/cilium_network_policy.h:52-71).
-// Quirks reproduced on purpose (each pinned by tests/test_regex_dfa.py against
-// std::regex in this container):
+// Quirks reproduced on purpose (pinned against std::regex in this container
+// by the differential fuzzer tests/cpp/fuzz_regex.cc, run from
+// tests/test_http_cpu.py::test_regex_compiler_differential_fuzz):
 //   * `\cX` is the character X (libstdc++ does not compute a control char);
 //   * `\uHHHH` keeps only the low byte; `\0` is NUL and stops (no octal);
 //   * `.` matches every byte except '\n' and '\r';

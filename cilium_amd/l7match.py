@@ -53,7 +53,8 @@ PROTO_KAFKA = 2
 HTTP_REC_FIXED = 20
 F_METHOD, F_PATH, F_AUTHORITY, F_INGRESS = 1, 2, 4, 8
 
-# Every symbol include/l7match.h declares (checked by tests/test_abi.py).
+# Every symbol include/l7match.h declares (checked by
+# tests/test_http_cpu.py::test_library_exports_every_header_symbol).
 EXPORTED_SYMBOLS = (
     "l7m_compile_http", "l7m_compile_kafka", "l7m_retain", "l7m_release",
     "l7m_ruleset_get_info", "l7m_ruleset_program", "l7m_http_translate",
@@ -62,7 +63,7 @@ EXPORTED_SYMBOLS = (
     "l7m_compile_http_policies", "l7m_ruleset_policy_index", "l7m_ruleset_rule_origin",
     "l7m_batcher_create", "l7m_batcher_set_ruleset", "l7m_batcher_eval", "l7m_batcher_eval_http",
     "l7m_batcher_stats", "l7m_batcher_destroy", "l7m_http_deny_body", "l7m_kafka_deny_response",
-    "l7m_proxy_stats_add",
+    "l7m_proxy_stats_add", "l7m_compile_kafka_map", "l7m_eval_ids", "l7m_eval_device_ids",
 )
 
 
@@ -82,6 +83,16 @@ class _KafkaRule(ctypes.Structure):
     _fields_ = [("role", ctypes.c_char_p), ("api_key", ctypes.c_char_p),
                 ("api_version", ctypes.c_char_p), ("client_id", ctypes.c_char_p),
                 ("topic", ctypes.c_char_p)]
+
+
+class _KafkaSelectorRules(ctypes.Structure):
+    _fields_ = [("rules", ctypes.POINTER(_KafkaRule)), ("n_rules", ctypes.c_size_t),
+                ("wildcard", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class _IdentitySelectors(ctypes.Structure):
+    _fields_ = [("identity", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("selectors", ctypes.POINTER(ctypes.c_uint32)), ("n_selectors", ctypes.c_size_t)]
 
 
 class _Opts(ctypes.Structure):
@@ -179,6 +190,11 @@ def _load() -> ctypes.CDLL:
                                      ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.l7m_compile_kafka.argtypes = [ctypes.POINTER(_KafkaRule), sz, ctypes.POINTER(_Opts),
                                       ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.l7m_compile_kafka_map.argtypes = [ctypes.POINTER(_KafkaSelectorRules), sz,
+                                          ctypes.POINTER(_IdentitySelectors), sz, ctypes.POINTER(_Opts),
+                                          ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.l7m_eval_ids.argtypes = [P, P, sz, P, sz, P, P, P, ctypes.c_uint32]
+    lib.l7m_eval_device_ids.argtypes = [P, P, sz, P, sz, P, P, P, P, ctypes.c_uint32]
     lib.l7m_compile_http_policies.argtypes = [ctypes.POINTER(_NetworkPolicy), sz, ctypes.POINTER(_Opts),
                                               ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.l7m_ruleset_policy_index.argtypes = [P, ctypes.c_char_p]
@@ -495,11 +511,38 @@ class RuleSet:
             raise L7Error(rc, "rule index out of range")
         return (o.policy, bool(o.ingress), o.port, o.port_rule, o.http_rule)
 
-    @classmethod
-    def compile_kafka(cls, rules: Sequence[PortRuleKafka]) -> "RuleSet":
-        arr = (_KafkaRule * max(1, len(rules)))(*[
+    @staticmethod
+    def _kafka_rules(rules: Sequence[PortRuleKafka]):
+        return (_KafkaRule * max(1, len(rules)))(*[
             _KafkaRule(_b(r.Role) or None, _b(r.APIKey) or None, _b(r.APIVersion) or None,
                        _b(r.ClientID) or None, _b(r.Topic) or None) for r in rules])
+
+    @classmethod
+    def compile_kafka_map(cls, entries: Sequence[Tuple[Sequence[PortRuleKafka], bool]],
+                          identities: Optional[dict] = None) -> "RuleSet":
+        """The Kafka redirect's L7DataMap (pkg/policy/l4.go:110-129): entries =
+        [(rules, is_wildcard_selector)], identities = {numeric identity:
+        [indices of the entries whose selector matches its labels]}.  Evaluate
+        with eval(..., identities=per-request source identities)."""
+        keep = [cls._kafka_rules(r) for r, _ in entries]
+        ents = (_KafkaSelectorRules * max(1, len(entries)))(*[
+            _KafkaSelectorRules(keep[i], len(r), 1 if w else 0, 0) for i, (r, w) in enumerate(entries)])
+        items = sorted((identities or {}).items())
+        sels = [(ctypes.c_uint32 * max(1, len(v)))(*v) for _, v in items]
+        ids = (_IdentitySelectors * max(1, len(items)))(*[
+            _IdentitySelectors(k, 0, sels[i], len(v)) for i, (k, v) in enumerate(items)])
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        opts = cls._opts(0, 0, 0)
+        rc = _lib.l7m_compile_kafka_map(ents, len(entries), ids, len(items), ctypes.byref(opts), ctypes.byref(out),
+                                        err, 1024)
+        if rc != L7M_OK:
+            raise L7Error(rc, err.value.decode(errors="replace"))
+        return cls(out.value, PROTO_KAFKA)
+
+    @classmethod
+    def compile_kafka(cls, rules: Sequence[PortRuleKafka]) -> "RuleSet":
+        arr = cls._kafka_rules(rules)
         out = ctypes.c_void_p()
         err = ctypes.create_string_buffer(1024)
         opts = cls._opts(0, 0, 0)
@@ -509,9 +552,10 @@ class RuleSet:
         return cls(out.value, PROTO_KAFKA)
 
     # ---- evaluation -------------------------------------------------------
-    def eval(self, arena: np.ndarray, offsets: np.ndarray, hits: Optional[np.ndarray] = None
-             ) -> np.ndarray:
-        """Host buffers -> int32 verdicts (H2D, kernel, D2H on the current device)."""
+    def eval(self, arena: np.ndarray, offsets: np.ndarray, hits: Optional[np.ndarray] = None,
+             identities: Optional[np.ndarray] = None) -> np.ndarray:
+        """Host buffers -> int32 verdicts (H2D, kernel, D2H on the current device).
+        identities: per-request source identity (Kafka rule sets, l7m_eval_ids)."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         n = offsets.shape[0]
@@ -520,8 +564,14 @@ class RuleSet:
         if hits is not None:
             assert hits.dtype == np.uint64 and hits.shape[0] >= self.n_counters
             hp = hits.ctypes.data
-        rc = _lib.l7m_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data, n,
-                           verdicts.ctypes.data, hp, 0)
+        if identities is not None:
+            identities = np.ascontiguousarray(identities, dtype=np.uint32)
+            assert identities.shape[0] == n
+            rc = _lib.l7m_eval_ids(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data, n,
+                                   identities.ctypes.data, verdicts.ctypes.data, hp, 0)
+        else:
+            rc = _lib.l7m_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data, n,
+                               verdicts.ctypes.data, hp, 0)
         if rc != L7M_OK:
             raise L7Error(rc, "l7m_eval failed")
         return verdicts

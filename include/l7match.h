@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define L7M_ABI_VERSION 2
+#define L7M_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define L7M_OK 0
@@ -70,7 +70,8 @@ extern "C" {
 /* ---- verdicts (int32 per request) --------------------------------------- */
 #define L7M_VERDICT_DENY (-1)         /* no rule allows the request               */
 #define L7M_VERDICT_PARSE_ERROR (-2)  /* Kafka: ReadRequest would return an error  */
-#define L7M_VERDICT_UNSUPPORTED (-3)  /* Kafka: compressed message set (gzip/snappy) */
+#define L7M_VERDICT_UNSUPPORTED (-3)  /* Kafka: a gzip/snappy message set past the second
+                                        pass's limits (nesting depth 8, slab, queue)     */
 #define L7M_VERDICT_ALLOW_NO_L7 (0x7fffffff) /* HTTP rule list empty: port has no L7
                                         rules, Envoy allows (cilium_network_policy.h:129-135) */
 #define L7M_VERDICT_ALLOW_NO_PORT_POLICY (0x7ffffffe) /* no per-port policy for the
@@ -165,6 +166,27 @@ typedef struct {
   const char* topic;
 } l7m_kafka_rule;
 
+/* The Kafka redirect's L7DataMap (pkg/policy/l4.go:110-129 GetRelevantRules):
+ * one entry per endpoint selector with that selector's PortRuleKafka rules.
+ * `wildcard` marks api.WildcardEndpointSelector, whose rules apply to every
+ * source; the others apply to the source identities whose labels the
+ * selector matches, listed per identity in an l7m_identity_selectors
+ * table; the control plane evaluates selector.Matches(labels).  At most 64
+ * entries. */
+typedef struct {
+  const l7m_kafka_rule* rules;
+  size_t n_rules;
+  uint32_t wildcard;
+  uint32_t reserved;
+} l7m_kafka_selector_rules;
+
+typedef struct {
+  uint32_t identity;          /* numeric security identity (!= 0)                 */
+  uint32_t reserved;
+  const uint32_t* selectors;  /* indices of the L7DataMap entries that select it  */
+  size_t n_selectors;
+} l7m_identity_selectors;
+
 typedef struct {
   uint32_t struct_size;     /* sizeof(l7m_opts); 0 = use defaults               */
   uint32_t dialect;         /* L7M_DIALECT_*                                    */
@@ -192,6 +214,16 @@ int l7m_compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts* opts,
                      l7m_ruleset** out, char* err, size_t errlen);
 int l7m_compile_kafka(const l7m_kafka_rule* rules, size_t n, const l7m_opts* opts,
                       l7m_ruleset** out, char* err, size_t errlen);
+/* canAccess with GetRelevantRules (pkg/proxy/kafka.go:116-152): a request
+ * from source identity s is decided by MatchesRule over the rules of the
+ * entries that select s (none when s == 0 or s is not listed: the reference's
+ * nil identity) followed by the wildcard entries' rules; no such rule ->
+ * deny.  Verdict indices number the rules entry by entry in `map` order.
+ * The source identities travel beside the arena (l7m_eval_ids);
+ * l7m_compile_kafka(rules, n) is the map of one wildcard entry. */
+int l7m_compile_kafka_map(const l7m_kafka_selector_rules* map, size_t n_entries,
+                          const l7m_identity_selectors* identities, size_t n_identities,
+                          const l7m_opts* opts, l7m_ruleset** out, char* err, size_t errlen);
 /* A NetworkPolicyMap of n endpoint policies.  A request names its policy by
  * index in the record (l7m_ruleset_policy_index; 0xffff = a name the map does
  * not hold -> deny, cilium_network_policy.h:231-235); its direction and dport
@@ -288,6 +320,14 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
              const uint64_t* rec_offsets, size_t n, int32_t* verdicts, uint64_t* rule_hits,
              uint32_t flags);
 
+/* l7m_eval with the source identity of every request (u32 per request; the
+ * redirect's srcIdentity, pkg/proxy/kafka.go:245).  Kafka rule sets only;
+ * src_identities == NULL is every request from identity 0.  HTTP records
+ * carry their remote identity themselves: L7M_EINVAL for HTTP rule sets. */
+int l7m_eval_ids(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
+                 const uint64_t* rec_offsets, size_t n, const uint32_t* src_identities,
+                 int32_t* verdicts, uint64_t* rule_hits, uint32_t flags);
+
 /* Device-resident variant: all pointers are device pointers on the current HIP
  * device; the work is enqueued on `hip_stream` (NULL = default stream) and the
  * call returns without synchronising.  d_arena must be 16-byte aligned and
@@ -296,6 +336,10 @@ int l7m_eval(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
 int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes,
                     const void* d_rec_offsets, size_t n, void* d_verdicts, void* d_rule_hits,
                     void* hip_stream, uint32_t flags);
+/* ... with device-resident source identities (see l7m_eval_ids). */
+int l7m_eval_device_ids(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes,
+                        const void* d_rec_offsets, size_t n, const void* d_src_identities,
+                        void* d_verdicts, void* d_rule_hits, void* hip_stream, uint32_t flags);
 
 /* ---- batching front-end (the call-site shape of the reference) ------------
  * canAccess (pkg/proxy/kafka.go:116-152) and AccessFilter::decodeHeaders

@@ -294,6 +294,18 @@ struct KRule {
 };
 struct KafkaOracle {
   std::vector<KRule> rules;
+  // L7DataMap (pkg/policy/l4.go:110-129): rule i belongs to entry group[i];
+  // a source's relevant entries are those whose selector matches it plus the
+  // wildcard entries.  !selective: one wildcard entry, every rule applies.
+  std::vector<uint32_t> group;
+  bool selective = false;
+  uint64_t wild = ~0ull;
+  std::map<uint32_t, uint64_t> id_mask;
+  uint64_t mask_of(uint32_t identity) const {
+    if (!selective) return ~0ull;
+    auto it = identity ? id_mask.find(identity) : id_mask.end();
+    return it == id_mask.end() ? wild : it->second;  // nil identity: wildcard entries only
+  }
 };
 
 const std::map<std::string, int16_t>& api_key_map() {
@@ -839,10 +851,13 @@ bool rule_matches(const KReq& q, const KRule& r) {
   return !(!r.topic.empty() && is_topic_api_key(q.kind));
 }
 
-int32_t eval_kafka_one(const KafkaOracle& o, const KReq& q) {
+// MatchesRule (policy.go:197-225) over GetRelevantRules' list: the rules
+// that apply to the source (mask), in compiled order.
+int32_t eval_kafka_one(const KafkaOracle& o, const KReq& q, uint64_t mask = ~0ull) {
   if (q.status) return q.status;
   std::set<std::string> left(q.topics.begin(), q.topics.end());
   for (size_t i = 0; i < o.rules.size(); ++i) {
+    if (o.selective && !((mask >> o.group[i]) & 1)) continue;
     const KRule& r = o.rules[i];
     if (r.topic.empty() || q.topics.empty()) {
       if (rule_matches(q, r)) return (int32_t)i;
@@ -1025,6 +1040,46 @@ int orc_kafka_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint
                    int32_t* verdicts, int threads) {
   const KafkaOracle& o = *static_cast<KafkaOracle*>(h);
   parallel_for(n, threads, [&](size_t i) { verdicts[i] = eval_kafka_one(o, parse_kafka(arena, arena_bytes, offs[i])); });
+  return L7M_OK;
+}
+
+// An L7DataMap: entries of (rules, wildcard) and, per source identity, the
+// entries whose selector matches it.
+int orc_kafka_new_map(const l7m_kafka_selector_rules* map, size_t n_entries, const l7m_identity_selectors* ids,
+                      size_t n_ids, void** out, char* err, size_t errlen) {
+  auto* o = new KafkaOracle();
+  o->wild = 0;
+  for (size_t g = 0; g < n_entries; ++g) {
+    if (map[g].wildcard) o->wild |= 1ull << g;
+    else o->selective = true;
+    for (size_t j = 0; j < map[g].n_rules; ++j) {
+      KRule r;
+      std::string e;
+      int rc = sanitize(map[g].rules[j], &r, &e);
+      if (rc) {
+        set_err(err, errlen, "rule " + std::to_string(o->rules.size()) + ": " + e);
+        delete o;
+        return rc;
+      }
+      o->rules.push_back(std::move(r));
+      o->group.push_back(static_cast<uint32_t>(g));
+    }
+  }
+  for (size_t k = 0; k < n_ids; ++k) {
+    uint64_t m = o->wild;
+    for (size_t j = 0; j < ids[k].n_selectors; ++j) m |= 1ull << ids[k].selectors[j];
+    o->id_mask[ids[k].identity] = m;
+  }
+  *out = o;
+  return L7M_OK;
+}
+
+int orc_kafka_eval_ids(void* h, const uint8_t* arena, size_t arena_bytes, const uint64_t* offs, size_t n,
+                       const uint32_t* ids, int32_t* verdicts, int threads) {
+  const KafkaOracle& o = *static_cast<KafkaOracle*>(h);
+  parallel_for(n, threads, [&](size_t i) {
+    verdicts[i] = eval_kafka_one(o, parse_kafka(arena, arena_bytes, offs[i]), o.mask_of(ids ? ids[i] : 0u));
+  });
   return L7M_OK;
 }
 

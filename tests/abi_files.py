@@ -21,11 +21,11 @@ def write_inputs(tmp, rules, arena, offs):
     return rp, qp
 
 
-def run(tmp, rules, arena, offs, threads, iters, timeout=240):
+def run(tmp, rules, arena, offs, threads, iters, timeout=240, batcher=False):
     rp, qp = write_inputs(tmp, rules, arena, offs)
     out = os.path.join(tmp, "out.bin")
-    p = subprocess.run([HARNESS, rp, qp, str(threads), str(iters), out], capture_output=True, text=True,
-                       timeout=timeout)
+    p = subprocess.run([HARNESS, rp, qp, str(threads), str(iters), out] + (["batcher"] if batcher else []),
+                       capture_output=True, text=True, timeout=timeout)
     res = None
     if os.path.exists(out):
         raw = open(out, "rb").read()

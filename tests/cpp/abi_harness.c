@@ -2,7 +2,7 @@
  * abi_harness.c — a plain C client of libl7match.so (no ctypes, no torch):
  * the binding a cgo shim or an Envoy filter would use.
  *
- *   abi_harness <rules.txt> <requests.bin> <threads> <iters> <out.bin>
+ *   abi_harness <rules.txt> <requests.bin> <threads> <iters> <out.bin> [batcher]
  *
  * rules.txt    one HTTP rule per line: path \t method \t host \t headers (\x1f-separated)
  * requests.bin u64 n, u64 arena_bytes, u64 offsets[n], arena bytes
@@ -13,6 +13,16 @@
  * call l7m_eval `iters` times concurrently on the SAME handle (the reentrancy
  * promise of include/l7match.h) and compare their verdicts with thread 0's.
  * Exit status 0 = every call succeeded and every thread saw identical verdicts.
+ *
+ * With the 6th argument `batcher`: the call-site shape instead.  One
+ * l7m_batcher over the handle; `threads` host threads each take every
+ * threads-th request and decide it with the blocking per-request
+ * l7m_batcher_eval (canAccess / decodeHeaders), while thread 0 swaps in a
+ * second compile of the same rules halfway (l7m_batcher_set_ruleset, the
+ * policy update).  Every denied request gets its 403 body
+ * (l7m_http_deny_body).  out.bin: i32 verdicts[n] by request index, then
+ * u64 {batches, requests, denied, forwarded} (l7m_batcher_stats and
+ * l7m_proxy_stats_add over the verdicts).
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -42,6 +52,76 @@ static void* run(void* arg) {
   return NULL;
 }
 
+typedef struct {
+  l7m_batcher* b;
+  l7m_ruleset* swap_to;  /* thread 0 only */
+  const uint8_t* arena;
+  const uint64_t* offs;
+  size_t n, arena_bytes;
+  int t, threads;
+  int32_t* verdicts;
+  int rc;
+} bjob_t;
+
+static void* run_batched(void* arg) {
+  bjob_t* j = (bjob_t*)arg;
+  char body[64];
+  for (size_t i = (size_t)j->t; i < j->n && j->rc == L7M_OK; i += (size_t)j->threads) {
+    if (j->swap_to && i >= j->n / 2) {
+      j->rc = l7m_batcher_set_ruleset(j->b, j->swap_to);
+      j->swap_to = NULL;
+      if (j->rc != L7M_OK) break;
+    }
+    const size_t end = i + 1 < j->n ? j->offs[i + 1] : j->arena_bytes;
+    j->rc = l7m_batcher_eval(j->b, j->arena + j->offs[i], (size_t)(end - j->offs[i]), &j->verdicts[i]);
+    if (j->rc == L7M_OK && j->verdicts[i] == L7M_VERDICT_DENY &&
+        l7m_http_deny_body("", body, sizeof body) != strlen("Access denied\r\n"))
+      j->rc = -100;
+  }
+  return NULL;
+}
+
+static int batched(l7m_ruleset* rs, l7m_ruleset* rs2, const uint8_t* arena, size_t ab, const uint64_t* offs,
+                   size_t n, int threads, const char* out) {
+  l7m_batcher* b = NULL;
+  l7m_batcher_opts o;
+  memset(&o, 0, sizeof o);
+  o.struct_size = sizeof o;
+  o.max_delay_us = 500;
+  if (l7m_batcher_create(rs, &o, &b) != L7M_OK) return 8;
+  int32_t* verd = (int32_t*)malloc(n * 4);
+  bjob_t* jobs = (bjob_t*)calloc((size_t)threads, sizeof(bjob_t));
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (bjob_t){b, t == 0 ? rs2 : NULL, arena, offs, n, ab, t, threads, verd, L7M_OK};
+    pthread_create(&th[t], NULL, run_batched, &jobs[t]);
+  }
+  int bad = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].rc != L7M_OK) {
+      fprintf(stderr, "thread %d: batcher %d\n", t, jobs[t].rc);
+      bad = 1;
+    }
+  }
+  uint64_t st[4] = {0, 0, 0, 0};
+  l7m_batcher_stats(b, &st[0], &st[1]);
+  l7m_batcher_destroy(b);
+  l7m_proxy_stats ps;
+  memset(&ps, 0, sizeof ps);
+  if (l7m_proxy_stats_add(verd, n, &ps) != L7M_OK) bad = 1;
+  st[2] = ps.denied;
+  st[3] = ps.forwarded;
+  FILE* f = fopen(out, "wb");
+  if (!f) return 7;
+  fwrite(verd, 4, n, f);
+  fwrite(st, 8, 4, f);
+  fclose(f);
+  printf("abi_harness: batcher, %zu requests, %d threads, %llu batches: %s\n", n, threads,
+         (unsigned long long)st[0], bad ? "FAILED" : "ok");
+  return bad;
+}
+
 static char* dup_range(const char* a, const char* b) {
   char* s = (char*)malloc((size_t)(b - a) + 1);
   memcpy(s, a, (size_t)(b - a));
@@ -50,8 +130,8 @@ static char* dup_range(const char* a, const char* b) {
 }
 
 int main(int argc, char** argv) {
-  if (argc != 6) {
-    fprintf(stderr, "usage: %s rules.txt requests.bin threads iters out.bin\n", argv[0]);
+  if (argc != 6 && !(argc == 7 && strcmp(argv[6], "batcher") == 0)) {
+    fprintf(stderr, "usage: %s rules.txt requests.bin threads iters out.bin [batcher]\n", argv[0]);
     return 2;
   }
   const int threads = atoi(argv[3]), iters = atoi(argv[4]);
@@ -123,6 +203,14 @@ int main(int argc, char** argv) {
   uint8_t* arena = (uint8_t*)malloc(ab);
   if (fread(offs, 8, n, f) != n || fread(arena, 1, ab, f) != ab) return 6;
   fclose(f);
+  if (argc == 7) {
+    l7m_ruleset* rs2 = NULL;
+    if (l7m_compile_http(rules, nr, NULL, &rs2, err, sizeof err) != L7M_OK) return 5;
+    const int r = batched(rs, rs2, arena, ab, offs, n, threads, argv[5]);
+    l7m_release(rs2);
+    l7m_release(rs);
+    return r;
+  }
   /* ---- concurrent evaluation on one handle ---- */
   job_t* jobs = (job_t*)calloc((size_t)threads, sizeof(job_t));
   pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));

@@ -30,6 +30,9 @@ def _load():
     lib.orc_kafka_new.argtypes = [ctypes.POINTER(L._KafkaRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.orc_kafka_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_kafka_free.argtypes = [P]
+    lib.orc_kafka_new_map.argtypes = [ctypes.POINTER(L._KafkaSelectorRules), sz, ctypes.POINTER(L._IdentitySelectors),
+                                      sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.orc_kafka_eval_ids.argtypes = [P, P, sz, P, sz, P, P, ctypes.c_int]
     lib.orc_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
     lib.orc_regex_search.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
     return lib
@@ -110,12 +113,37 @@ class KafkaOracle:
         if getattr(self, "_h", None) and self._h.value:
             _lib.orc_kafka_free(self._h)
 
-    def eval(self, arena, offsets, threads=1):
+    @classmethod
+    def from_map(cls, entries, identities=None):
+        """L7DataMap oracle: entries = [(rules, is_wildcard)], identities =
+        {identity: [entry indices whose selector matches it]}."""
+        self = cls.__new__(cls)
+        keep = [L.RuleSet._kafka_rules(r) for r, _ in entries]
+        ents = (L._KafkaSelectorRules * max(1, len(entries)))(*[
+            L._KafkaSelectorRules(keep[i], len(r), 1 if w else 0, 0) for i, (r, w) in enumerate(entries)])
+        items = sorted((identities or {}).items())
+        sels = [(ctypes.c_uint32 * max(1, len(v)))(*v) for _, v in items]
+        ids = (L._IdentitySelectors * max(1, len(items)))(*[
+            L._IdentitySelectors(k, 0, sels[i], len(v)) for i, (k, v) in enumerate(items)])
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        rc = _lib.orc_kafka_new_map(ents, len(entries), ids, len(items), ctypes.byref(h), err, 512)
+        if rc != 0:
+            raise OracleError(rc, err.value.decode(errors="replace"))
+        self._h = h
+        return self
+
+    def eval(self, arena, offsets, threads=1, identities=None):
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         v = np.empty(offsets.shape[0], dtype=np.int32)
-        _lib.orc_kafka_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
-                            offsets.shape[0], v.ctypes.data, threads)
+        if identities is None:
+            _lib.orc_kafka_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
+                                offsets.shape[0], v.ctypes.data, threads)
+        else:
+            identities = np.ascontiguousarray(identities, dtype=np.uint32)
+            _lib.orc_kafka_eval_ids(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
+                                    offsets.shape[0], identities.ctypes.data, v.ctypes.data, threads)
         return v
 
 

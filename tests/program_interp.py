@@ -20,7 +20,7 @@ CR_REMOTE = 0x80000000
 HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_dfa off_dfas off_fields "
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
-              "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi pf_dfa").split()
+              "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off").split()
 
@@ -47,7 +47,7 @@ class HttpProgram:
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
         h = self.h
         assert h["magic"] == 0x3448374C
-        assert len(HDR_FIELDS) == 33
+        assert len(HDR_FIELDS) == 32
         io = h["lds_image_off"]
         self.img = self.w[io:io + h["lds_image_words"]]
         self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
@@ -81,17 +81,29 @@ class HttpProgram:
         """Packed double-array walk (cilium_amd/csrc/dfa_pack.h): end code."""
         d = self.dfas[k]
         lds = d["lds_table"] != KNONE
-        T, Toff = (self.img, d["lds_table"]) if lds else (self.w, d["table_off"])
         base = d["start_base"]
         last = KNONE
-        for b in data:
-            if not base:
-                break
-            slot = base + b
-            e = T[Toff + slot]
-            if base < d["region"]:
-                last = slot
-            base = e >> 8 if (e & 0xFF) == b else 0
+        if lds:
+            # LDS copy (program.h kLdsRowShift): e = (image row index << 16) | label,
+            # the table's row 0 is the dead row
+            t0 = d["lds_table"]
+            for b in data:
+                if not base:
+                    break
+                slot = base + b
+                e = self.img[t0 + slot]
+                if base < d["region"]:
+                    last = slot
+                base = (e >> 16) - t0 if (e & 0xFFFF) == b else 0
+        else:
+            for b in data:
+                if not base:
+                    break
+                slot = base + b
+                e = self.w[d["table_off"] + slot]
+                if base < d["region"]:
+                    last = slot
+                base = e >> 8 if (e & 0xFF) == b else 0
         if not base:
             return 0
         if lds and d["lds_es"] != KNONE:  # table-only LDS placement keeps end codes in the program

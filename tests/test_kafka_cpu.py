@@ -88,3 +88,36 @@ def test_config3_generator_and_oracle_sample():
     arena, offs = W.requests(3, 0, 5000, n_rules=2000)
     v = KafkaOracle(rules).eval(arena, offs)
     assert (v >= 0).any() and (v == -1).any() and not (v <= -2).any()
+
+
+def test_l7datamap_oracle_allows_exactly_what_getrelevantrules_allows():
+    """The map oracle (rules filtered by the source's selector mask, in
+    compiled order) allows or denies exactly as MatchesRule over the list
+    GetRelevantRules builds for that source (selecting entries, then the
+    wildcard entries appended)."""
+    import selector_cases as S
+    entries, ids = S.random_map(3, n_rules=600, n_ids=12)
+    arena, offs = W.requests(3, 7_000_000, 3000, n_rules=600)
+    idv = S.request_identities(5, len(offs), ids)
+    got = KafkaOracle.from_map(entries, ids).eval(arena, offs, threads=8, identities=idv)
+    for ident in np.unique(idv).tolist():
+        sel = np.nonzero(idv == ident)[0]
+        sub_a, sub_o = L.pack_records([bytes(arena[offs[i]:(offs[i + 1] if i + 1 < len(offs) else arena.nbytes)])
+                                       for i in sel])
+        ref = KafkaOracle(S.relevant_rules(entries, ids, ident)).eval(sub_a, sub_o)
+        assert np.array_equal(got[sel] >= 0, ref >= 0), ident
+        assert np.array_equal(got[sel] <= -2, ref <= -2), ident
+    assert (got >= 0).any() and (got == -1).any()
+
+
+def test_l7datamap_compile_errors():
+    r = [L.PortRuleKafka(Topic="t")]
+    with pytest.raises(L.L7Error) as e:
+        L.RuleSet.compile_kafka_map([(r, False)] * 65)
+    assert e.value.code == L.L7M_ETOOBIG
+    for ids in ({0: [0]}, {5: [3]}):
+        with pytest.raises(L.L7Error) as e:
+            L.RuleSet.compile_kafka_map([(r, False), (r, True)], ids)
+        assert e.value.code == L.L7M_EINVAL
+    L.RuleSet.compile_kafka_map([(r, False), (r, True)], {5: [0]})
+    L.RuleSet.compile_kafka_map([], {})

@@ -156,3 +156,29 @@ def test_many_rules_global_counters_parity(gpu):
     recs = K.random_requests(rng, 20000, topics[:3000] + ["nope"], ["client-%d" % i for i in range(60)])
     arena, offs = L.pack_records(recs)
     _check(rules, arena, offs, hits=True)
+
+
+def test_l7datamap_source_identities_parity(gpu):
+    """GetRelevantRules on the GPU: a 6-entry L7DataMap (2 wildcard entries),
+    40 identities with random selector matches, requests from listed,
+    unlisted and unresolved (0) sources: verdicts and counters bit-exact
+    with the map oracle; without identities every source is unresolved."""
+    import selector_cases as S
+    entries, ids = S.random_map(11)
+    arena, offs = W.requests(3, 9_000_000, 60_000, n_rules=1200)
+    idv = S.request_identities(13, len(offs), ids)
+    rs = L.RuleSet.compile_kafka_map(entries, ids)
+    orc = KafkaOracle.from_map(entries, ids)
+    h = np.zeros(rs.n_counters, dtype=np.uint64)
+    got = rs.eval(arena, offs, h, identities=idv)
+    exp = orc.eval(arena, offs, threads=8, identities=idv)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(idv[i]), int(exp[i]), int(got[i])) for i in bad[:10]]
+    assert int(h[0]) == int((exp == -1).sum()) and int(h.sum()) == len(exp)
+    assert (exp >= 0).any() and (exp == -1).any()
+    none = rs.eval(arena, offs)
+    assert np.array_equal(none, orc.eval(arena, offs, threads=8, identities=np.zeros(len(offs), np.uint32)))
+    # a map of one wildcard entry is l7m_compile_kafka
+    rules = [r for e, _ in entries for r in e]
+    assert np.array_equal(L.RuleSet.compile_kafka_map([(rules, True)]).eval(arena, offs, identities=idv),
+                          L.RuleSet.compile_kafka(rules).eval(arena, offs))

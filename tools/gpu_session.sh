@@ -19,7 +19,7 @@ for s in "$@"; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
            rc=$?; [ $rc -le 1 ] || exit $rc ;;
-    tests:*) step pytest_${s#tests:} 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#tests:}"
+    tests:*) step pytest_sel 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#tests:}"
            rc=$?; [ $rc -le 1 ] || exit $rc ;;
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench:*) step bench_${s#bench:} 600 python -u bench.py --config ${s#bench:} || exit $? ;;
@@ -27,6 +27,9 @@ for s in "$@"; do
     prof:*) c=${s#prof:}; step prof_$c 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_$c -o run --output-format csv -- python3 -u bench.py --config $c --steps 20 --warmup 2 --no-cpu-baseline || exit $? ;;
     pmc:*) c=${s#pmc:}; cfg=${c%%:*}; ctr=${c#*:}
            step pmc_${cfg}_$ctr 300 rocprofv3 --pmc $ctr -d $PWD/$OUT/pmc_${cfg}_$ctr -o run --output-format csv -- python3 -u bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline || exit $? ;;
+    vtests:*) v=${s#vtests:}; name=${v%%:*}; kx=${v#*:}
+           L7M_LIB=variants/$name.so step vtests_$name 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$kx"
+           rc=$?; [ $rc -le 1 ] || exit $rc ;;
     var:*) v=${s#var:}; name=${v%%:*}; cfg=${v#*:}
            L7M_LIB=variants/$name.so step var_${name}_$cfg 300 python -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
