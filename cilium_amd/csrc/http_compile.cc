@@ -542,7 +542,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     const uint64_t half_es = (d.n_slots + 1) / 2, half_latch = (d.latch.size() + 1) / 2;
     const uint64_t need = ((d.n_slots + 3) & ~3ull) + ((half_es + 3) & ~3ull) + ((half_latch + 3) & ~3ull);
     const bool es16 = d.sets.size() < kEs16Latched && all[k].npats < kEs16Latched;
-    if (es16 && img + need <= budget) {
+    const bool es8 = d.sets.size() < kEs8Latched && all[k].npats < kEs16Latched;
+    const uint64_t need8 = ((d.n_slots + 3) & ~3ull) + ((half_latch + 3) & ~3ull);
+    if (es8 && img + need8 <= budget) {  // end codes ride in the slot entries
+      dd[k].lds_table = img_take(d.n_slots);
+      dd[k].lds_es = kLdsEsInEntry;
+      dd[k].lds_latch = 2 * img_take(half_latch);
+    } else if (es16 && img + need <= budget) {
       dd[k].lds_table = img_take(d.n_slots);
       dd[k].lds_es = 2 * img_take(half_es);
       dd[k].lds_latch = 2 * img_take(half_latch);
@@ -645,13 +651,20 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     }
     if (!ce.empty()) std::memcpy(P + dd[k].ct_off, ce.data(), ce.size() * sizeof(CandEntry));
     if (dd[k].lds_table != kNone) {
-      // the LDS copy names rows by image word index (program.h kLdsRowShift)
+      // the LDS copy names rows by image word index (program.h kLdsRowShift),
+      // with the target state's end code when it fits 8 bits
       const uint32_t t0 = dd[k].lds_table;
+      const bool in_entry = dd[k].lds_es == kLdsEsInEntry;
+      auto es8 = [&](uint32_t base) -> uint32_t {
+        return d.es[base] == kLatchedAccept ? kEs8Latched : d.es[base];
+      };
       for (uint32_t s = 0; s < d.n_slots; ++s) {
         const uint32_t e = d.table[s], next = e >> 8;
-        I[t0 + s] = next ? ((t0 + next) << kLdsRowShift) | (e & 0xffu) : (t0 << kLdsRowShift);
+        I[t0 + s] = next ? ((t0 + next) << kLdsRowShift) | (in_entry ? es8(next) << 8 : 0u) | (e & 0xffu)
+                         : (t0 << kLdsRowShift);
       }
-      for (uint32_t s = 0; dd[k].lds_es != kNone && s < d.n_slots; ++s)
+      if (in_entry && d.start_base) dd[k].start_es8 = es8(d.start_base);
+      for (uint32_t s = 0; dd[k].lds_es != kNone && !in_entry && s < d.n_slots; ++s)
         I16[dd[k].lds_es + s] = d.es[s] == kLatchedAccept ? static_cast<uint16_t>(kEs16Latched)
                                                            : static_cast<uint16_t>(d.es[s]);
       for (size_t s = 0; dd[k].lds_latch != kNone && s < d.latch.size(); ++s)

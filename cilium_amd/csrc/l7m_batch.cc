@@ -31,6 +31,7 @@ using Clock = std::chrono::steady_clock;
 struct Batch {
   std::vector<uint8_t> arena;
   std::vector<uint64_t> offs;
+  std::vector<uint32_t> ids;  // source identities (Kafka rule sets)
   std::vector<int32_t> verd;
   Clock::time_point first;
   bool done = false;
@@ -69,8 +70,11 @@ struct l7m_batcher {
       lk.unlock();
       b->verd.resize(b->offs.size());
       b->arena.resize(b->arena.size() + 64, 0);  // tail padding for aligned loads
-      const int rc = l7m_eval(r, b->arena.data(), b->arena.size() - 64, b->offs.data(), b->offs.size(),
-                              b->verd.data(), nullptr, 0);
+      l7m_ruleset_info info;
+      l7m_ruleset_get_info(r, &info);
+      const int rc = l7m_eval_ids(r, b->arena.data(), b->arena.size() - 64, b->offs.data(), b->offs.size(),
+                                  info.proto == L7M_PROTO_KAFKA ? b->ids.data() : nullptr, b->verd.data(), nullptr,
+                                  0);
       l7m_release(r);
       lk.lock();
       b->rc = rc;
@@ -79,7 +83,7 @@ struct l7m_batcher {
     }
   }
 
-  int eval(const uint8_t* rec, size_t len, int32_t* verdict) {
+  int eval(const uint8_t* rec, size_t len, uint32_t src_identity, int32_t* verdict) {
     std::unique_lock<std::mutex> lk(mu);
     if (stop) return L7M_EINVAL;
     std::shared_ptr<Batch> b = cur;
@@ -87,6 +91,7 @@ struct l7m_batcher {
     if (idx == 0) b->first = Clock::now();
     const size_t off = b->arena.size();
     b->offs.push_back(off);
+    b->ids.push_back(src_identity);
     b->arena.resize(off + ((len + 3) & ~size_t(3)), 0);
     if (len) std::memcpy(b->arena.data() + off, rec, len);
     if (idx == 0 || b->offs.size() >= max_batch) cv_flush.notify_one();
@@ -133,7 +138,12 @@ int l7m_batcher_set_ruleset(l7m_batcher* b, l7m_ruleset* rs) {
 
 int l7m_batcher_eval(l7m_batcher* b, const uint8_t* rec, size_t len, int32_t* verdict) {
   if (!b || (!rec && len) || !verdict) return L7M_EINVAL;
-  return b->eval(rec, len, verdict);
+  return b->eval(rec, len, 0, verdict);
+}
+
+int l7m_batcher_eval_from(l7m_batcher* b, const uint8_t* rec, size_t len, uint32_t src_identity, int32_t* verdict) {
+  if (!b || (!rec && len) || !verdict) return L7M_EINVAL;
+  return b->eval(rec, len, src_identity, verdict);
 }
 
 int l7m_batcher_eval_http(l7m_batcher* b, const l7m_http_request* req, int32_t* verdict) {
@@ -143,7 +153,7 @@ int l7m_batcher_eval_http(l7m_batcher* b, const l7m_http_request* req, int32_t* 
   std::vector<uint8_t> rec(sz);
   uint64_t off = 0;
   if (l7m_pack_http(req, 1, rec.data(), rec.size(), &off) != sz) return L7M_EINVAL;
-  return b->eval(rec.data(), rec.size(), verdict);
+  return b->eval(rec.data(), rec.size(), 0, verdict);
 }
 
 int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests) {

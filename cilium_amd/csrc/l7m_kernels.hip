@@ -118,7 +118,7 @@ struct LdsChain {
   __device__ __forceinline__ void init(const DfaDesc& dd) {
     dead = dd.lds_table << kLdsRowShift;
     lim = dd.lds_table + dd.region;
-    sel = (dd.lds_table + dd.start_base) << kLdsRowShift;
+    sel = ((dd.lds_table + dd.start_base) << kLdsRowShift) | (dd.start_es8 << 8);
     slast = kNone;
   }
   __device__ __forceinline__ void step(const uint32_t* __restrict__ img, uint32_t b) {
@@ -126,7 +126,7 @@ struct LdsChain {
     asm("" : "+v"(s));  // one SDWA add, then the scale
     const uint32_t e = img[s];
     slast = (sel >> kLdsRowShift) < lim ? s : slast;
-    sel = (e & 0xffffu) == b ? e : dead;
+    sel = (e & 0xffu) == b ? e : dead;
   }
   __device__ __forceinline__ bool dead_now() const { return sel == dead; }
   // continue the walk over bytes [k, len) of the field at pos
@@ -140,7 +140,15 @@ struct LdsChain {
   __device__ __forceinline__ uint32_t code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
                                            const DfaDesc& dd) const {
     const uint32_t t0 = dead >> kLdsRowShift;
-    return end_code<true>(img, prog, dd, (sel >> kLdsRowShift) - t0, slast == kNone ? kNone : slast - t0);
+    const uint32_t base = (sel >> kLdsRowShift) - t0, last = slast == kNone ? kNone : slast - t0;
+    if (dd.lds_es == kLdsEsInEntry) {  // the end code came with the last entry read
+      if (!base) return 0;
+      const uint32_t es = (sel >> 8) & 0xffu;
+      if (es != kEs8Latched) return es;
+      const uint16_t* I16 = reinterpret_cast<const uint16_t*>(img);
+      return kLatchedBit | (last == kNone ? dd.start_latch : I16[dd.lds_latch + last]);
+    }
+    return end_code<true>(img, prog, dd, base, last);
   }
 };
 

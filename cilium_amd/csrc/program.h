@@ -67,7 +67,8 @@ struct DfaDesc {
   uint32_t nstates;
   uint32_t lds_ctmask;   // LDS image word offset of a bitmask: ct entry i has candidates, or kNone
   uint32_t ctmask_off;   // program: the same bitmask (always)
-  uint32_t pad[4];
+  uint32_t start_es8;    // lds_es == kLdsEsInEntry: the start state's end code (es8)
+  uint32_t pad[3];
 };
 static_assert(sizeof(DfaDesc) == 96, "dfa desc is 24 words");
 
@@ -90,6 +91,12 @@ constexpr uint32_t kEs16Latched = 0xffffu;
 // unowned slot) = lds_table << kLdsRowShift (the table's row 0, where no
 // label matches).  The image is < 64 Ki words (kLdsBytes), so indices fit.
 constexpr uint32_t kLdsRowShift = 16;
+// When a DFA has fewer than 255 end codes its LDS entries also carry the end
+// code of the state they lead to: entry = row << 16 | es8 << 8 | label, es8 =
+// es (0 = no match) or kEs8Latched; its lds_es is then kLdsEsInEntry and the
+// walk needs no end-code table (start_es8: the start state's).
+constexpr uint32_t kLdsEsInEntry = 0xfffffffeu;
+constexpr uint32_t kEs8Latched = 0xffu;
 
 // ---- HTTP kernel geometry and LDS budget -------------------------------
 // Shared by the compiler's LDS image sizing (http_compile.cc) and the kernel

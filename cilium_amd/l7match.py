@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "l7m_batcher_create", "l7m_batcher_set_ruleset", "l7m_batcher_eval", "l7m_batcher_eval_http",
     "l7m_batcher_stats", "l7m_batcher_destroy", "l7m_http_deny_body", "l7m_kafka_deny_response",
     "l7m_proxy_stats_add", "l7m_compile_kafka_map", "l7m_eval_ids", "l7m_eval_device_ids",
+    "l7m_batcher_eval_from",
 )
 
 
@@ -201,6 +202,7 @@ def _load() -> ctypes.CDLL:
     lib.l7m_batcher_create.argtypes = [P, ctypes.POINTER(_BatcherOpts), ctypes.POINTER(P)]
     lib.l7m_batcher_set_ruleset.argtypes = [P, P]
     lib.l7m_batcher_eval.argtypes = [P, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int32)]
+    lib.l7m_batcher_eval_from.argtypes = [P, ctypes.c_char_p, sz, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]
     lib.l7m_batcher_eval_http.argtypes = [P, ctypes.POINTER(_HttpReq), ctypes.POINTER(ctypes.c_int32)]
     lib.l7m_batcher_stats.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     lib.l7m_batcher_destroy.argtypes = [P]
@@ -633,9 +635,9 @@ class Batcher:
         self.ruleset = ruleset
         _lib.l7m_batcher_set_ruleset(self._h, ruleset.handle)
 
-    def eval(self, record: bytes) -> int:
+    def eval(self, record: bytes, src_identity: int = 0) -> int:
         v = ctypes.c_int32()
-        rc = _lib.l7m_batcher_eval(self._h, record, len(record), ctypes.byref(v))
+        rc = _lib.l7m_batcher_eval_from(self._h, record, len(record), src_identity, ctypes.byref(v))
         if rc != L7M_OK:
             raise L7Error(rc, "l7m_batcher_eval failed")
         return v.value

@@ -361,6 +361,10 @@ int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batche
 int l7m_batcher_set_ruleset(l7m_batcher* b, l7m_ruleset* rs);
 /* One request (a record as in the arena); blocks until its batch is decided. */
 int l7m_batcher_eval(l7m_batcher* b, const uint8_t* record, size_t len, int32_t* verdict);
+/* ... from source identity src_identity (canAccess's srcIdentity; Kafka rule
+ * sets compiled from an L7DataMap, see l7m_eval_ids; ignored for HTTP). */
+int l7m_batcher_eval_from(l7m_batcher* b, const uint8_t* record, size_t len, uint32_t src_identity,
+                          int32_t* verdict);
 int l7m_batcher_eval_http(l7m_batcher* b, const l7m_http_request* req, int32_t* verdict);
 int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests);
 void l7m_batcher_destroy(l7m_batcher* b);

@@ -22,7 +22,8 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
               "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
-              "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off").split()
+              "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8").split()
+ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 
 
 def name_hash(data: bytes) -> int:
@@ -83,9 +84,10 @@ class HttpProgram:
         lds = d["lds_table"] != KNONE
         base = d["start_base"]
         last = KNONE
+        es8 = d["start_es8"]
         if lds:
-            # LDS copy (program.h kLdsRowShift): e = (image row index << 16) | label,
-            # the table's row 0 is the dead row
+            # LDS copy (program.h kLdsRowShift): e = (image row index << 16) |
+            # es8 << 8 | label, the table's row 0 is the dead row
             t0 = d["lds_table"]
             for b in data:
                 if not base:
@@ -94,7 +96,7 @@ class HttpProgram:
                 e = self.img[t0 + slot]
                 if base < d["region"]:
                     last = slot
-                base = (e >> 16) - t0 if (e & 0xFFFF) == b else 0
+                base, es8 = ((e >> 16) - t0, (e >> 8) & 0xFF) if (e & 0xFF) == b else (0, 0)
         else:
             for b in data:
                 if not base:
@@ -106,6 +108,10 @@ class HttpProgram:
                 base = e >> 8 if (e & 0xFF) == b else 0
         if not base:
             return 0
+        if lds and d["lds_es"] == ES_IN_ENTRY:
+            if es8 != 0xFF:
+                return es8
+            return LATCHED | (d["start_latch"] if last == KNONE else self.img16[d["lds_latch"] + last])
         if lds and d["lds_es"] != KNONE:  # table-only LDS placement keeps end codes in the program
             es = self.img16[d["lds_es"] + base]
             if es != ES16_LATCHED:

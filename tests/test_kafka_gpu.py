@@ -182,3 +182,40 @@ def test_l7datamap_source_identities_parity(gpu):
     rules = [r for e, _ in entries for r in e]
     assert np.array_equal(L.RuleSet.compile_kafka_map([(rules, True)]).eval(arena, offs, identities=idv),
                           L.RuleSet.compile_kafka(rules).eval(arena, offs))
+
+
+def test_batcher_kafka_l7datamap_threads(gpu):
+    """canAccess's call shape: 8 threads decide Kafka requests one at a time
+    through one batcher (l7m_batcher_eval_from with the source identity) on
+    an L7DataMap rule set; a policy update (set_ruleset) lands midway;
+    verdicts equal the map oracle's."""
+    import threading
+    import selector_cases as S
+    entries, ids = S.random_map(17, n_rules=800, n_ids=16)
+    arena, offs = W.requests(3, 11_000_000, 4000, n_rules=800)
+    idv = S.request_identities(19, len(offs), ids)
+    exp = KafkaOracle.from_map(entries, ids).eval(arena, offs, threads=8, identities=idv)
+    buf = arena.tobytes()
+    ends = list(offs[1:].tolist()) + [len(buf)]
+    got = np.zeros(len(offs), dtype=np.int32)
+    b = L.Batcher(L.RuleSet.compile_kafka_map(entries, ids), max_delay_us=300)
+    errs = []
+
+    def run(t):
+        try:
+            for i in range(t, len(offs), 8):
+                if t == 0 and i == (len(offs) // 16) * 8:
+                    b.set_ruleset(L.RuleSet.compile_kafka_map(entries, ids))
+                got[i] = b.eval(buf[offs[i]:ends[i]], int(idv[i]))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    th = [threading.Thread(target=run, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    batches, requests = b.stats()
+    b.close()
+    assert not errs, errs
+    assert np.array_equal(got, exp)
+    assert requests == len(offs) and batches < requests
