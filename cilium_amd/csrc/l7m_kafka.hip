@@ -35,6 +35,8 @@
 namespace l7m {
 namespace {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // A view of a byte range with the optiopay decoder's sticky-error semantics:
 // a short read consumes what is left (io.ReadFull) and sets err.
 struct Rd {
@@ -532,7 +534,6 @@ constexpr uint32_t kKMaxLdsCounters = 16384;
 constexpr uint32_t kSpanLds = (4 * kKafkaKinds + 3) & ~3u;  // words
 constexpr uint32_t kKindOkLds = (2 * kKafkaKinds + 3) & ~3u;  // words
 constexpr uint32_t kMaxCliLdsBytes = 8192;  // client table copied to LDS up to this size
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
   const uint32_t lo = __shfl(static_cast<uint32_t>(x), src);
