@@ -601,6 +601,22 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     h.name_len_lo = static_cast<uint32_t>(m);
     h.name_len_hi = static_cast<uint32_t>(m >> 32);
   }
+  {
+    // DFAs / fields the verification must visit (uniform skips in the kernel)
+    uint64_t cm = 0, pm = 0;
+    for (uint32_t k = 0; k < ndfa && k < 64; ++k)
+      for (const Span& sp : ct[k])
+        if (sp.len) {
+          cm |= 1ull << k;
+          break;
+        }
+    for (uint32_t f = 0; f < nf; ++f)
+      if (fd[f].presence.len) pm |= 1ull << f;
+    h.cand_dfas_lo = static_cast<uint32_t>(cm);
+    h.cand_dfas_hi = static_cast<uint32_t>(cm >> 32);
+    h.pres_fields_lo = static_cast<uint32_t>(pm);
+    h.pres_fields_hi = static_cast<uint32_t>(pm >> 32);
+  }
   h.n_policies = plan.n_policies;
   h.ent_mask = ent_slots - 1;
   h.ent_tab_off = take(2ull * ent_slots);
@@ -610,6 +626,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     dd[k].table_off = take(all[k].d->n_slots);
     dd[k].es_off = take(all[k].d->n_slots);
     dd[k].latch_off = take(all[k].d->latch.size());
+    w = (w + 15) & ~uint64_t(15);  // candidate entries on 64-byte boundaries
     dd[k].ct_off = take(16 * ct[k].size());
     dd[k].ctmask_off = take((ct[k].size() + 31) / 32);
   }

@@ -15,7 +15,7 @@ namespace l7m {
 // program.h name hash of a host string (Kafka topic / ClientID tables, HTTP
 // header-name table).
 inline uint32_t name_hash(const std::string& s) {
-  const size_t words = std::max<size_t>(kNameHashMinWords, (s.size() + 3) / 4);
+  const size_t words = (s.size() + 3) / 4;
   uint32_t h = 0;
   for (size_t k = 0; k < words; ++k) {
     uint32_t w = 0;

@@ -213,10 +213,13 @@ __device__ __forceinline__ Name load_name(const uint8_t* t, uint32_t len) {
   uint32_t h = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kNameWords; ++k) {
-    const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-    const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
-    nm.x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
-    h = name_hash_step(h, nm.x[k]);
+    nm.x[k] = 0;
+    if (__any(4 * k < len)) {  // words past every lane's name are skipped
+      const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+      const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
+      nm.x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+      if (rem > 0) h = name_hash_step(h, nm.x[k]);
+    }
   }
   for (uint32_t i = 4 * kNameWords; i < len; i += 4) {  // names longer than 24 bytes
     uint32_t x = 0;

@@ -256,10 +256,13 @@ __device__ __forceinline__ uint32_t name_field_of(const Ctx& c, const HttpHeader
   uint32_t hh = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kW; ++k) {
-    const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-    const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
-    x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
-    hh = name_hash_step(hh, x[k]);
+    x[k] = 0;
+    if (__any(4 * k < len)) {  // words past every lane's name are skipped
+      const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+      const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
+      x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+      if (rem > 0) hh = name_hash_step(hh, x[k]);
+    }
   }
   for (uint32_t i = 4 * kW; i < len; i += 4) {  // names longer than 24 bytes
     uint32_t y = 0;
@@ -385,37 +388,29 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   HPROF(1);
   uint64_t present = 0;
   codes.clear(h.n_dfas);
+  // Walk jobs, one loop so that the walk code exists once in the kernel
+  // (instruction-cache footprint): 0 method, 1 path, 2 authority, 3 + j the
+  // value of header j when a rule references its name (first occurrence).
+  // The job index is wave-uniform; lanes with fewer headers drop out.
   uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
-  auto eval_field = [&](uint32_t f, uint32_t p, uint32_t len) {
-    const FieldDesc& fd = c.fields[f];
-    for (uint32_t k = 0; k < fd.ndfa; ++k) {
-      const uint32_t d = fd.dfa_first + k;
-      codes.set(d, walk_dfa(c, d, src, p, len));
-    }
-  };
-  if (flags & L7M_HTTP_F_METHOD) {
-    present |= 1ull << kFieldMethod;
-    eval_field(kFieldMethod, pos, mlen);
-  }
-  HPROF(2);
-  pos += mlen;
-  if (flags & L7M_HTTP_F_PATH) {
-    present |= 1ull << kFieldPath;
-    eval_field(kFieldPath, pos, plen);
-  }
-  HPROF(3);
-  pos += plen;
-  if (flags & L7M_HTTP_F_AUTHORITY) {
-    present |= 1ull << kFieldAuthority;
-    eval_field(kFieldAuthority, pos, alen);
-  }
-  HPROF(4);
-  pos += alen;
-  if (h.has_name_dfa) {
-    for (uint32_t j = 0; j < nhdr; ++j) {
-      const uint32_t e = src.word(5 + j);
+  const uint32_t njobs = 3u + (h.has_name_dfa ? nhdr : 0u);
+  // DFAs with candidate entries (a uniform mask when n_dfas <= 64)
+  const bool masked = h.n_dfas <= 64;
+  const uint64_t cand_all = masked ? ((static_cast<uint64_t>(h.cand_dfas_hi) << 32) | h.cand_dfas_lo) : 0;
+  // The candidate entry (program memory) of the first walk that selects one
+  // is touched (one dword load) as soon as that walk ends, so its L2 round
+  // trip overlaps the remaining walks and verification reads the entry from
+  // the CU's L1 (the walks in between touch no global memory).
+  uint32_t pf_d = kNone, pf_t = 0;
+  for (uint32_t job = 0; job < njobs; ++job) {
+    uint32_t f = kNone, p = pos, len;
+    if (job < 3) {
+      len = job == 0 ? mlen : job == 1 ? plen : alen;
+      if (flags & (job == 0 ? L7M_HTTP_F_METHOD : job == 1 ? L7M_HTTP_F_PATH : L7M_HTTP_F_AUTHORITY)) f = job;
+      pos += len;
+    } else {
+      const uint32_t e = src.word(5 + job - 3);
       const uint32_t nl = e & 0xffffu, vl = e >> 16;
-      uint32_t f = kNone;
       const uint32_t lb = nl < 63 ? nl : 63;
       if (!(((lb < 32 ? h.name_len_lo >> lb : h.name_len_hi >> (lb - 32)) & 1u))) {
         // no rule references a header name of this length
@@ -426,11 +421,27 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
         if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
         else if (code) f = c.name_field[code];
       }
-      if (f != kNone && !((present >> f) & 1ull)) {  // first occurrence wins
-        present |= 1ull << f;
-        eval_field(f, pos + nl, vl);
-      }
+      if (f != kNone && ((present >> f) & 1ull)) f = kNone;  // first occurrence wins
+      p = pos + nl;
+      len = vl;
       pos += nl + vl;
+    }
+    if (f != kNone) {
+      present |= 1ull << f;
+      const FieldDesc& fd = c.fields[f];
+      for (uint32_t k = 0; k < fd.ndfa; ++k) {
+        const uint32_t d = fd.dfa_first + k;
+        const uint32_t code = walk_dfa(c, d, src, p, len);
+        codes.set(d, code);
+        if (pf_d == kNone && code && ((cand_all >> d) & 1ull)) {
+          const DfaDesc& dd = c.dds[d];
+          if (dd.lds_ct == kNone) {
+            const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
+            pf_t = c.prog[dd.ct_off + 16u * idx];
+            pf_d = d;
+          }
+        }
+      }
     }
   }
 
@@ -503,21 +514,33 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     const u32x4* q = reinterpret_cast<const u32x4*>(e);
     check_entry(q[0], q[1], q[2]);
   };
-  for (uint32_t d = 0; d < h.n_dfas; ++d) {
+  asm volatile("" ::"v"(pf_t));  // the touch completes here, not at its first use
+  (void)pf_d;
+  // only DFAs with candidate entries
+  uint64_t cm = cand_all;
+  for (uint32_t i = 0; masked ? cm != 0 : i < h.n_dfas; ++i) {
+    uint32_t d = i;
+    if (masked) {
+      d = static_cast<uint32_t>(__builtin_ctzll(cm));
+      cm &= cm - 1;
+    }
     const uint32_t code = codes.get(d);
     if (!code) continue;
     const DfaDesc& dd = c.dds[d];
     const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
     const uint32_t mw = dd.lds_ctmask != kNone ? c.img[dd.lds_ctmask + (idx >> 5)] : c.prog[dd.ctmask_off + (idx >> 5)];
     if (!((mw >> (idx & 31u)) & 1u)) continue;  // no candidates
-    if (dd.lds_ct != kNone) check_inline(c.img + dd.lds_ct + 16u * idx);
-    else check_inline(c.prog + dd.ct_off + 16u * idx);
-  }
-  for (uint32_t f = 0; f < h.n_fields; ++f)
-    if ((present >> f) & 1ull) {
-      const Span cl = c.fields[f].presence;
-      if (cl.len) scan(cl);
+    if (dd.lds_ct != kNone) {
+      check_inline(c.img + dd.lds_ct + 16u * idx);
+    } else {
+      check_inline(c.prog + dd.ct_off + 16u * idx);
     }
+  }
+  for (uint64_t pm = ((static_cast<uint64_t>(h.pres_fields_hi) << 32) | h.pres_fields_lo) & present; pm;
+       pm &= pm - 1) {
+    const uint32_t f = static_cast<uint32_t>(__builtin_ctzll(pm));
+    scan(c.fields[f].presence);
+  }
   if (h.zero_list.len) scan(h.zero_list);
   HPROF(6);
 

@@ -171,7 +171,10 @@ struct HttpHeader {
   uint32_t ent_mask;       // its slot count - 1
   uint32_t name_len_lo;    // bit l (l < 64, 63 = longer) set iff a referenced header
   uint32_t name_len_hi;    // name has that length: other names skip the lookup
-  uint32_t pad[4];         // header = 36 words
+  uint32_t cand_dfas_lo;   // bit d (n_dfas <= 64): value DFA d has candidate
+  uint32_t cand_dfas_hi;   // entries for some end code (else verification skips it)
+  uint32_t pres_fields_lo; // bit f: field f has a presence-keyed check-record list
+  uint32_t pres_fields_hi;  // header = 36 words
 };
 // Header-name table (LDS image): exact lower-case header names of the rules
 // -> field id, open addressing on the program.h name hash; slot =
@@ -276,16 +279,17 @@ static_assert(sizeof(KafkaTopicExt) == 16, "topic ext is 4 words");
 static_assert(sizeof(KafkaClientSlot) == 32, "client slot is 8 words");
 static_assert(sizeof(KafkaHeader) % 16 == 0, "header is whole 16-byte lines");
 
-// Key hash of the Kafka topic / ClientID tables: the name zero-padded to
-// max(len, 24) rounded up to whole words, read as little-endian u32 words,
-// each folded in by a multiply-rotate step (word-wise so that the device
-// hashes the 24-byte prefix it already holds in registers without byte
-// extraction); the length is mixed in last and 0 is remapped (0 marks an
-// empty slot).
+// Key hash of the Kafka topic / ClientID tables and the HTTP header-name
+// table: the name as ceil(len / 4) little-endian u32 words (the last one zero
+// padded), each folded in by a step of full-rate VALU operations (xor, a 24-bit
+// multiply-add, a rotate: no quarter-rate 32-bit multiply per word), then a
+// murmur3 finalizer over the length; 0 is remapped (0 marks an empty slot).
+// Device code hashes the first kNameHashMinWords words from registers it
+// already holds for the compare, word-wise without byte extraction.
 constexpr uint32_t kNameHashMinWords = 6;
 __host__ __device__ inline uint32_t name_hash_step(uint32_t h, uint32_t w) {
-  h = (h ^ w) * 0x9e3779b1u;
-  return h ^ (h >> 15);
+  const uint32_t x = h ^ w;
+  return (x & 0xffffffu) * 0x9e3779u + ((x << 13) | (x >> 19));
 }
 __host__ __device__ inline uint32_t name_hash_final(uint32_t h, uint32_t len) {
   h = (h ^ len) * 0x85ebca6bu;

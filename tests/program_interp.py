@@ -29,12 +29,11 @@ ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 def name_hash(data: bytes) -> int:
     """program.h name_hash_step / name_hash_final."""
     M = 0xFFFFFFFF
-    words = max(6, (len(data) + 3) // 4)
     h = 0
-    for k in range(words):
+    for k in range((len(data) + 3) // 4):
         w = int.from_bytes(data[4 * k:4 * k + 4].ljust(4, b"\0"), "little")
-        h = ((h ^ w) * 0x9E3779B1) & M
-        h ^= h >> 15
+        x = h ^ w
+        h = ((x & 0xFFFFFF) * 0x9E3779 + (((x << 13) | (x >> 19)) & M)) & M
     h = ((h ^ len(data)) * 0x85EBCA6B) & M
     h ^= h >> 13
     h = (h * 0xC2B2AE35) & M

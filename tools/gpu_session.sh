@@ -30,6 +30,10 @@ for s in "$@"; do
     vtests:*) v=${s#vtests:}; name=${v%%:*}; kx=${v#*:}
            L7M_LIB=variants/$name.so step vtests_$name 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$kx"
            rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    diag:*) v=${s#diag:}; cfg=${v%%:*}; mode=${v#*:}
+           step diag_${cfg}_$mode 300 python -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --diag $mode || exit $? ;;
+    envb:*) v=${s#envb:}; name=${v%%:*}; rest=${v#*:}; cfg=${rest%%:*}; kv=${rest#*:}
+           step envb_${name}_$cfg 300 env $kv python -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
     var:*) v=${s#var:}; name=${v%%:*}; cfg=${v#*:}
            L7M_LIB=variants/$name.so step var_${name}_$cfg 300 python -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
