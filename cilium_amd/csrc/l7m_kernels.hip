@@ -329,17 +329,30 @@ __device__ __forceinline__ uint32_t ent_lookup(const Ctx& c, const HttpHeader& h
   } while (0)
 #endif
 
-// Full evaluation of one record whose first `limit` bytes are readable.
+// What the walk phase of a record hands to its verification phase.
+template <bool kReg>
+struct WalkOut {
+  Codes<kReg> codes;  // end code per value DFA
+  uint64_t present;   // fields present in the request
+  uint32_t ex, e0;    // port entries whose rules may decide (exact port, port 0)
+  uint32_t remote;    // the request's remote identity
+  uint32_t pf_t;      // the candidate-entry touch (kept live until verification)
+  bool h0;            // the port-0 entry has HTTP rules
+};
+constexpr int32_t kNeedVerify = INT32_MIN;
+
+// Walk phase of one record whose first `limit` bytes are readable: record
+// validation, port-entry selection and every DFA walk.  Returns the verdict
+// when it is decided without rules, else kNeedVerify with `o` filled in.
 // kAblate (diagnostic builds selected by L7M_FLAG_DIAG_*; verdicts invalid):
 // 1 = stop after the DFA walks, 2 = stop after record validation.
 template <bool kReg, int kAblate, class Src>
-__device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit,
-                                               uint32_t* col PROF_PARAM) {
+__device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit,
+                                             WalkOut<kReg>& o PROF_PARAM) {
 #ifdef L7M_PROF
   if (Src::kLds) prof[0] = __builtin_amdgcn_s_memtime();
 #endif
-  Codes<kReg> codes;
-  if constexpr (!kReg) codes.p = col;
+  Codes<kReg>& codes = o.codes;
   if (limit < L7M_HTTP_REC_FIXED) return L7M_VERDICT_PARSE_ERROR;
   const uint32_t w0 = src.word(0), w1 = src.word(1), w2 = src.word(2), w3 = src.word(3), w4 = src.word(4);
   const uint32_t flags = (w2 >> 16) & 0xffu;
@@ -380,20 +393,17 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
       h0 = (vx != kNone && v0 != kNone) ? (v0 & kEntHaveHttp) != 0 : true;
     }
   }
-  // a rule may decide only if it belongs to ex, or to e0 when e0 has HTTP rules
-  auto eligible = [&](uint32_t hd) -> bool {
-    const uint32_t e = cr_entry(hd);
-    return e == ex || (h0 && e == e0);
-  };
   HPROF(1);
   uint64_t present = 0;
   codes.clear(h.n_dfas);
   // Walk jobs, one loop so that the walk code exists once in the kernel
-  // (instruction-cache footprint): 0 method, 1 path, 2 authority, 3 + j the
-  // value of header j when a rule references its name (first occurrence).
-  // The job index is wave-uniform; lanes with fewer headers drop out.
+  // (instruction-cache footprint): 0 method, 1 path, 2 authority, then the
+  // values of headers whose name a rule references (first occurrence).  The
+  // job index is wave-uniform; for the header jobs each lane first moves its
+  // cursor (hj, hp) past headers whose name length no rule uses, so a wave
+  // runs one job per referenced header, not one per header.
   uint32_t pos = L7M_HTTP_REC_FIXED + 4u * nhdr;
-  const uint32_t njobs = 3u + (h.has_name_dfa ? nhdr : 0u);
+  uint32_t hj = 0, hp = pos + mlen + plen + alen;
   // DFAs with candidate entries (a uniform mask when n_dfas <= 64)
   const bool masked = h.n_dfas <= 64;
   const uint64_t cand_all = masked ? ((static_cast<uint64_t>(h.cand_dfas_hi) << 32) | h.cand_dfas_lo) : 0;
@@ -402,29 +412,38 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
   // trip overlaps the remaining walks and verification reads the entry from
   // the CU's L1 (the walks in between touch no global memory).
   uint32_t pf_d = kNone, pf_t = 0;
-  for (uint32_t job = 0; job < njobs; ++job) {
-    uint32_t f = kNone, p = pos, len;
+  (void)pf_d;
+  for (uint32_t job = 0;; ++job) {
+    uint32_t f = kNone, p = pos, len = 0;
     if (job < 3) {
       len = job == 0 ? mlen : job == 1 ? plen : alen;
       if (flags & (job == 0 ? L7M_HTTP_F_METHOD : job == 1 ? L7M_HTTP_F_PATH : L7M_HTTP_F_AUTHORITY)) f = job;
       pos += len;
     } else {
-      const uint32_t e = src.word(5 + job - 3);
-      const uint32_t nl = e & 0xffffu, vl = e >> 16;
-      const uint32_t lb = nl < 63 ? nl : 63;
-      if (!(((lb < 32 ? h.name_len_lo >> lb : h.name_len_hi >> (lb - 32)) & 1u))) {
-        // no rule references a header name of this length
-      } else if (h.lds_name_tab != kNone) {
-        f = name_field_of(c, h, src, pos, nl);
-      } else {
-        const uint32_t code = walk_dfa(c, h.n_dfas, src, pos, nl);
-        if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
-        else if (code) f = c.name_field[code];
+      if (!h.has_name_dfa) break;
+      uint32_t e = 0;
+      for (; hj < nhdr; ++hj) {
+        e = src.word(5 + hj);
+        const uint32_t nl = e & 0xffffu, lb = nl < 63 ? nl : 63;
+        if ((lb < 32 ? h.name_len_lo >> lb : h.name_len_hi >> (lb - 32)) & 1u) break;
+        hp += nl + (e >> 16);  // no rule references a header name of this length
       }
-      if (f != kNone && ((present >> f) & 1ull)) f = kNone;  // first occurrence wins
-      p = pos + nl;
-      len = vl;
-      pos += nl + vl;
+      if (!__any(hj < nhdr)) break;
+      if (hj < nhdr) {
+        const uint32_t nl = e & 0xffffu, vl = e >> 16;
+        if (h.lds_name_tab != kNone) {
+          f = name_field_of(c, h, src, hp, nl);
+        } else {
+          const uint32_t code = walk_dfa(c, h.n_dfas, src, hp, nl);
+          if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
+          else if (code) f = c.name_field[code];
+        }
+        if (f != kNone && ((present >> f) & 1ull)) f = kNone;  // first occurrence wins
+        p = hp + nl;
+        len = vl;
+        hp += nl + vl;
+        ++hj;
+      }
     }
     if (f != kNone) {
       present |= 1ull << f;
@@ -451,10 +470,32 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     for (uint32_t d = 0; d < h.n_dfas; ++d) acc += codes.get(d);
     return static_cast<int32_t>(acc & 7u);
   }
-  // First matching rule (smallest index) among the keyed candidates: walk
-  // the check-record lists selected by the end codes.
+  o.present = present;
+  o.ex = ex;
+  o.e0 = e0;
+  o.h0 = h0;
+  o.remote = w1;
+  o.pf_t = pf_t;
+  return kNeedVerify;
+}
+
+// Verification phase: the first rule (smallest index) among the keyed
+// candidates whose other matchers, port entry and remote set hold; the
+// check-record lists are selected by the walks' end codes.
+template <bool kReg>
+__device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o) {
+  const Codes<kReg>& codes = o.codes;
+  const uint64_t present = o.present;
+  const uint32_t ex = o.ex, e0 = o.e0, remote = o.remote;
+  const bool h0 = o.h0;
+  // a rule may decide only if it belongs to ex, or to e0 when e0 has HTTP rules
+  auto eligible = [&](uint32_t hd) -> bool {
+    const uint32_t e = cr_entry(hd);
+    return e == ex || (h0 && e == e0);
+  };
+  const bool masked = h.n_dfas <= 64;
+  const uint64_t cand_all = masked ? ((static_cast<uint64_t>(h.cand_dfas_hi) << 32) | h.cand_dfas_lo) : 0;
   uint32_t best = h.always_rule;
-  const uint32_t remote = w1;
   auto remote_ok = [&](uint32_t rid) -> bool {  // PortNetworkPolicyRule::Matches (h:92-97)
     const Span rr = c.remotes[rid];
     uint32_t lo = 0, hi = rr.len;
@@ -514,8 +555,7 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     const u32x4* q = reinterpret_cast<const u32x4*>(e);
     check_entry(q[0], q[1], q[2]);
   };
-  asm volatile("" ::"v"(pf_t));  // the touch completes here, not at its first use
-  (void)pf_d;
+  asm volatile("" ::"v"(o.pf_t));  // the touch completes here, not at its first use
   // only DFAs with candidate entries
   uint64_t cm = cand_all;
   for (uint32_t i = 0; masked ? cm != 0 : i < h.n_dfas; ++i) {
@@ -542,7 +582,6 @@ __device__ __forceinline__ int32_t eval_record(const Ctx& c, const HttpHeader& h
     scan(c.fields[f].presence);
   }
   if (h.zero_list.len) scan(h.zero_list);
-  HPROF(6);
 
   if (best != kNone) return static_cast<int32_t>(best);
   // the exact-port entry matched nothing; a port-0 entry without HTTP rules allows
@@ -664,9 +703,6 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
       if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
     }
     wave_sync();
-    const Tile t2 = plan(t.cur + t.take, o2, n2);
-    issue_bytes(t2);
-    load_offs(t2.cur + t2.take, &o2, &n2);
 
     const uint64_t o = t.o, onext = t.onext, base = t.base;
     const uint32_t k = t.k, take = t.take;
@@ -674,21 +710,32 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
 #ifdef L7M_PROF
     const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
+    WalkOut<kReg> wo;
+    if constexpr (!kReg) wo.codes.p = mycol;
     if (lane < take) {
       bool done = false;
       if (lane < k && onext - o >= L7M_HTTP_REC_FIXED) {
         const LdsSrc s{reinterpret_cast<const uint32_t*>(stg + (o - base))};
         const uint32_t w0 = s.word(0);
         if (((static_cast<uint64_t>(w0) + 3) & ~3ull) <= onext - o) {
-          v = eval_record<kReg, kAblate>(c, h, s, onext - o, mycol PROF_ARG);
+          v = eval_walk<kReg, kAblate>(c, h, s, onext - o, wo PROF_ARG);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: read HBM directly
         const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
         const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-        v = inb ? eval_record<kReg, kAblate>(c, h, s, arena_bytes - o, mycol PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
+        v = inb ? eval_walk<kReg, kAblate>(c, h, s, arena_bytes - o, wo PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
       }
+    }
+    // The next tile's bytes are requested only now, after the walks: they
+    // land during verification without holding kCopyIters x 4 registers
+    // through the walks (the walks read LDS only).
+    const Tile t2 = plan(t.cur + t.take, o2, n2);
+    issue_bytes(t2);
+    load_offs(t2.cur + t2.take, &o2, &n2);
+    if (lane < take) {
+      if (v == kNeedVerify) v = eval_verify<kReg>(c, h, wo);
       verdicts[t.cur + lane] = v;
     }
 #ifdef L7M_PROF
