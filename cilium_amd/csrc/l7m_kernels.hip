@@ -189,10 +189,10 @@ __device__ __forceinline__ void count_slot(unsigned long long* __restrict__ hits
 // Per-lane DFA end codes: in registers when the program has few value DFAs
 // (static-index select chains, no scratch), else in an LDS column.
 constexpr uint32_t kRegDfas = kHttpRegDfas;
-template <bool kReg>
+template <int kReg>
 struct Codes;
 template <>
-struct Codes<true> {
+struct Codes<8> {
   // eight named registers: an array here is turned back into scratch memory
   uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
   __device__ __forceinline__ void clear(uint32_t) { r0 = r1 = r2 = r3 = r4 = r5 = r6 = r7 = 0; }
@@ -213,7 +213,22 @@ struct Codes<true> {
   }
 };
 template <>
-struct Codes<false> {
+struct Codes<4> {  // programs with <= 4 value DFAs: four registers
+  uint32_t r0, r1, r2, r3;
+  __device__ __forceinline__ void clear(uint32_t) { r0 = r1 = r2 = r3 = 0; }
+  __device__ __forceinline__ void set(uint32_t d, uint32_t v) {
+    r0 = d == 0 ? v : r0;
+    r1 = d == 1 ? v : r1;
+    r2 = d == 2 ? v : r2;
+    r3 = d == 3 ? v : r3;
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t d) const {
+    const uint32_t a = d & 1 ? r1 : r0, b = d & 1 ? r3 : r2;
+    return d & 2 ? b : a;
+  }
+};
+template <>
+struct Codes<0> {
   uint32_t* p;  // LDS, stride kBlock
   __device__ __forceinline__ void clear(uint32_t n) {
     for (uint32_t d = 0; d < n; ++d) p[d * kBlock] = 0;
@@ -330,7 +345,7 @@ __device__ __forceinline__ uint32_t ent_lookup(const Ctx& c, const HttpHeader& h
 #endif
 
 // What the walk phase of a record hands to its verification phase.
-template <bool kReg>
+template <int kReg>
 struct WalkOut {
   Codes<kReg> codes;  // end code per value DFA
   uint64_t present;   // fields present in the request
@@ -346,7 +361,7 @@ constexpr int32_t kNeedVerify = INT32_MIN;
 // when it is decided without rules, else kNeedVerify with `o` filled in.
 // kAblate (diagnostic builds selected by L7M_FLAG_DIAG_*; verdicts invalid):
 // 1 = stop after the DFA walks, 2 = stop after record validation.
-template <bool kReg, int kAblate, class Src>
+template <int kReg, int kAblate, class Src>
 __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit,
                                              WalkOut<kReg>& o PROF_PARAM) {
 #ifdef L7M_PROF
@@ -413,6 +428,16 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
   // the CU's L1 (the walks in between touch no global memory).
   uint32_t pf_d = kNone, pf_t = 0;
   (void)pf_d;
+  auto touch = [&](uint32_t d, uint32_t code) {
+    if (pf_d == kNone && code && ((cand_all >> d) & 1ull)) {
+      const DfaDesc& dd = c.dds[d];
+      if (dd.lds_ct == kNone) {
+        const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
+        pf_t = c.prog[dd.ct_off + 16u * idx];
+        pf_d = d;
+      }
+    }
+  };
   for (uint32_t job = 0;; ++job) {
     uint32_t f = kNone, p = pos, len = 0;
     if (job < 3) {
@@ -452,14 +477,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         const uint32_t d = fd.dfa_first + k;
         const uint32_t code = walk_dfa(c, d, src, p, len);
         codes.set(d, code);
-        if (pf_d == kNone && code && ((cand_all >> d) & 1ull)) {
-          const DfaDesc& dd = c.dds[d];
-          if (dd.lds_ct == kNone) {
-            const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
-            pf_t = c.prog[dd.ct_off + 16u * idx];
-            pf_d = d;
-          }
-        }
+        touch(d, code);
       }
     }
   }
@@ -482,7 +500,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
 // Verification phase: the first rule (smallest index) among the keyed
 // candidates whose other matchers, port entry and remote set hold; the
 // check-record lists are selected by the walks' end codes.
-template <bool kReg>
+template <int kReg>
 __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o) {
   const Codes<kReg>& codes = o.codes;
   const uint64_t present = o.present;
@@ -603,14 +621,14 @@ __device__ __forceinline__ void wave_sync() {
 // end (small rule sets), or wave-aggregated global atomics.
 enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
 
-template <int kHits, bool kReg, int kAblate>
+template <int kHits, int kReg, int kAblate>
 __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,
                                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                            const uint64_t* __restrict__ offs, uint64_t n,
                                                            int32_t* __restrict__ verdicts,
                                                            unsigned long long* __restrict__ hits, uint32_t stage) {
   extern __shared__ __align__(16) uint32_t smem[];
-  const HttpHeader h = *reinterpret_cast<const HttpHeader*>(prog);
+  const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   uint32_t* img = smem;
   const uint32_t n_ctr = h.n_rules + 2;
@@ -795,7 +813,7 @@ uint32_t http_stage_bytes(const HttpHeader& h) {
   return static_cast<uint32_t>(s > kMaxStage ? kMaxStage : s);
 }
 
-template <int kHits, bool kReg, int kAblate = 0>
+template <int kHits, int kReg, int kAblate = 0>
 static hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, uint32_t stage) {
@@ -825,22 +843,23 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   if (flags & (L7M_FLAG_DIAG_WALK_ONLY | L7M_FLAG_DIAG_COPY_ONLY)) {  // diagnostic ablations
     if (!reg) return hipErrorInvalidValue;
     if (flags & L7M_FLAG_DIAG_COPY_ONLY)
-      return launch_one<kNoHits, true, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
-    return launch_one<kNoHits, true, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
+      return launch_one<kNoHits, 8, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
+    return launch_one<kNoHits, 8, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
   }
   const int mode = !hits ? kNoHits : (h.n_rules + 2 <= kMaxLdsCounters ? kLdsHits : kGlobalHits);
+  // end codes in 4 or 8 registers, or in LDS columns
 #define L7M_LAUNCH(M, R) \
   return launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage)
-  if (mode == kNoHits) {
-    if (reg) L7M_LAUNCH(kNoHits, true);
-    L7M_LAUNCH(kNoHits, false);
+#define L7M_LAUNCH_R(M)                 \
+  {                                     \
+    if (h.n_dfas <= 4) L7M_LAUNCH(M, 4); \
+    if (reg) L7M_LAUNCH(M, 8);          \
+    L7M_LAUNCH(M, 0);                   \
   }
-  if (mode == kLdsHits) {
-    if (reg) L7M_LAUNCH(kLdsHits, true);
-    L7M_LAUNCH(kLdsHits, false);
-  }
-  if (reg) L7M_LAUNCH(kGlobalHits, true);
-  L7M_LAUNCH(kGlobalHits, false);
+  if (mode == kNoHits) L7M_LAUNCH_R(kNoHits);
+  if (mode == kLdsHits) L7M_LAUNCH_R(kLdsHits);
+  L7M_LAUNCH_R(kGlobalHits);
+#undef L7M_LAUNCH_R
 #undef L7M_LAUNCH
 }
 
