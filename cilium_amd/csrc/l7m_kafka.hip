@@ -202,7 +202,7 @@ struct Name {
 // kLds: t is in the LDS stage, where reading past the name is harmless, so
 // all seven words are read unconditionally; from HBM only the words that
 // hold name bytes are.
-template <bool kLds>
+template <bool kLds, bool kHash = true>
 __device__ __forceinline__ Name load_name(const uint8_t* t, uint32_t len) {
   Name nm;
   const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(t)) & 3u;
@@ -218,9 +218,11 @@ __device__ __forceinline__ Name load_name(const uint8_t* t, uint32_t len) {
       const uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
       const int32_t rem = static_cast<int32_t>(len) - static_cast<int32_t>(4 * k);
       nm.x[k] = rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
-      if (rem > 0) h = name_hash_step(h, nm.x[k]);
+      if (kHash && rem > 0) h = name_hash_step(h, nm.x[k]);
     }
   }
+  nm.hash = 0;
+  if (!kHash) return nm;
   for (uint32_t i = 4 * kNameWords; i < len; i += 4) {  // names longer than 24 bytes
     uint32_t x = 0;
     for (uint32_t b = 0; b < 4 && i + b < len; ++b) x |= static_cast<uint32_t>(t[i + b]) << (8 * b);
@@ -500,11 +502,48 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       const uint64_t tr0 = __builtin_amdgcn_s_memtime();
       if (kLds) g_prof_dec += tr0 - g_prof_t0;
 #endif
-      for (uint32_t r = 0; r < nq && maxf != kNone; ++r) {
-        const uint32_t toff = tq[64 * r];
-        const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
-        const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid, gmask);
-        maxf = f > maxf ? f : maxf;
+      // The parked topics' home-slot heads (hash, meta, first rule) are
+      // fetched together, so the lookups of a request cost one dependent
+      // L2 round trip instead of one per topic; the second pass compares
+      // names against the slots' inline prefixes (same cache line).
+      uint32_t hs[kTopicQ];
+      u32x4 hd[kTopicQ];
+#pragma unroll
+      for (uint32_t r = 0; r < kTopicQ; ++r) {
+        hs[r] = 0;
+        hd[r] = u32x4{0u, 0u, 0u, 0u};
+        if (r < nq && maxf != kNone) {
+          const uint32_t toff = tq[64 * r];
+          const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
+          if (tlen && tlen <= kMaxTopicLen && v.n_slots) {
+            hs[r] = load_name<kLds>(rec + toff, tlen).hash;
+            hd[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[0];
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < kTopicQ; ++r) {
+        if (r < nq && maxf != kNone) {
+          uint32_t f = kNone;
+          if (hs[r] && hd[r].x != 0) {
+            const uint32_t toff = tq[64 * r];
+            const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
+            const uint32_t at = hs[r] & (v.n_slots - 1);
+            KafkaTopicSlot sl;
+            sl.hash = hd[r].x;
+            sl.meta = hd[r].y;
+            sl.r0 = hd[r].z;
+            sl.r0_client = hd[r].w;
+            const u32x4 pf = reinterpret_cast<const u32x4*>(v.slots + at)[1];
+            sl.pfx[0] = pf.x;
+            sl.pfx[1] = pf.y;
+            sl.pfx[2] = pf.z;
+            sl.pfx[3] = pf.w;
+            const Name nm = load_name<kLds, false>(rec + toff, tlen);
+            f = probe_topic(v, sl, hs[r], nm, rec + toff, tlen, kok, kind, version, cid, gmask);
+          }
+          maxf = f > maxf ? f : maxf;
+        }
       }
       const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid, gmask);
       first = j < maxf ? j : maxf;
