@@ -34,6 +34,8 @@ for s in "$@"; do
            step diag_${cfg}_$mode 300 python -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --diag $mode || exit $? ;;
     envb:*) v=${s#envb:}; name=${v%%:*}; rest=${v#*:}; cfg=${rest%%:*}; kv=${rest#*:}
            step envb_${name}_$cfg 300 env $kv python -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+    bargs:*) v=${s#bargs:}; name=${v%%:*}; rest=${v#*:}; cfg=${rest%%:*}; extra=${rest#*:}
+           step bargs_${name}_$cfg 300 python -u bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline ${extra//,/ } || exit $? ;;
     var:*) v=${s#var:}; name=${v%%:*}; cfg=${v#*:}
            L7M_LIB=variants/$name.so step var_${name}_$cfg 300 python -u bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
