@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/l7match.h"
 #include "l7m_device.h"
 #include "l7m_kcodec.h"
@@ -114,6 +116,43 @@ __device__ __forceinline__ void rd_skip_bytes(Rd& d) {
   }
   d.pos += static_cast<uint32_t>(n);
 }
+
+// Branch-free forms of the readers for records staged in LDS, where reading
+// up to 8 bytes past a range is harmless (the next record or the stage's
+// 16-byte slack): the bytes are read unconditionally and the sticky-error
+// state is updated with selects, so lanes whose reads fail do not split the
+// wave's control flow.  Same results as the readers above.
+struct RdL {
+  __device__ static __forceinline__ uint64_t be(Rd& d, uint32_t n) {
+    const bool ok = !d.err && d.len - d.pos >= n;
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < n; ++i) v = (v << 8) | d.p[d.pos + i];
+    d.err = !ok;
+    d.pos = ok ? d.pos + n : d.len;
+    return ok ? v : 0;
+  }
+  __device__ static __forceinline__ void skip(Rd& d, uint32_t n) {
+    const bool ok = !d.err && d.len - d.pos >= n;
+    d.err = !ok;
+    d.pos = ok ? d.pos + n : d.len;
+  }
+  __device__ static __forceinline__ void str(Rd& d, uint32_t* off, uint32_t* len) {
+    const bool was = d.err;
+    const int16_t n = static_cast<int16_t>(be(d, 2));
+    const bool valid = !d.err && n >= 1;
+    const bool fits = valid && d.len - d.pos >= static_cast<uint32_t>(n);
+    *off = fits ? d.pos : 0u;
+    *len = fits ? static_cast<uint32_t>(n) : 0u;
+    d.err = was || d.err || (valid && !fits);
+    d.pos = fits ? d.pos + static_cast<uint32_t>(n) : (valid ? d.len : d.pos);
+  }
+};
+// The branchy readers (any source, e.g. records read from HBM).
+struct RdG {
+  __device__ static __forceinline__ uint64_t be(Rd& d, uint32_t n) { return rd_be(d, n); }
+  __device__ static __forceinline__ void skip(Rd& d, uint32_t n) { rd_skip(d, n); }
+  __device__ static __forceinline__ void str(Rd& d, uint32_t* off, uint32_t* len) { rd_str(d, off, len); }
+};
 
 enum { kMsOk = 0, kMsErr = 1 };
 
@@ -373,6 +412,13 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
   const int16_t version = static_cast<int16_t>((rec[6] << 8) | rec[7]);  // request.go:72-74
   const uint32_t kidx = (kind >= 0 && kind < 64) ? static_cast<uint32_t>(kind) : 64u;
 
+  using R = typename std::conditional<kLds, RdL, RdG>::type;
+  auto arraylen = [](Rd& d, int32_t* n) -> bool {  // DecodeArrayLen (serialization.go:155-163)
+    const int32_t v = static_cast<int32_t>(R::be(d, 4));
+    if (v < 0 || v > kKafkaMaxParseBuf) return false;
+    *n = v;
+    return true;
+  };
   uint32_t first = kNone;
   const bool typed = kind == 0 || kind == 1 || kind == 2 || kind == 3 || kind == 8 || kind == 9 || kind == 10;
   if (!typed) {
@@ -383,7 +429,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
   } else {
     Rd d{rec, 4u + static_cast<uint32_t>(msize), 12, false};
     uint32_t coff, clen;
-    rd_str(d, &coff, &clen);
+    R::str(d, &coff, &clen);
     const uint8_t* client = rec + coff;
 #ifdef L7M_PROF
     const uint64_t tc0 = __builtin_amdgcn_s_memtime();
@@ -400,7 +446,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     auto start_topics = [&](int32_t n) { ntop = n; };
     auto topic = [&]() {
       uint32_t toff, tlen;
-      rd_str(d, &toff, &tlen);
+      R::str(d, &toff, &tlen);
       if (d.err || maxf == kNone) return;
       if (!tlen) {
         maxf = kNone;
@@ -423,35 +469,35 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     uint32_t a, b;
     switch (kind) {
       case 0:  // ReadProduceReq messages.go:1572-1628
-        if (version >= 3) rd_str(d, &a, &b);  // transactional id
-        rd_skip(d, 2 + 4);                    // acks, timeout
+        if (version >= 3) R::str(d, &a, &b);  // transactional id
+        R::skip(d, 2 + 4);                    // acks, timeout
         break;
       case 1:  // ReadFetchReq messages.go:752-809
-        rd_skip(d, 12 + (version >= 3 ? 4 : 0) + (version >= 4 ? 1 : 0));
+        R::skip(d, 12 + (version >= 3 ? 4 : 0) + (version >= 4 ? 1 : 0));
         break;
       case 2:  // ReadOffsetReq messages.go:1791-1839
-        rd_skip(d, 4 + (version >= 2 ? 1 : 0));
+        R::skip(d, 4 + (version >= 2 ? 1 : 0));
         break;
       case 8:  // ReadOffsetCommitReq messages.go:1158-1213
-        rd_str(d, &a, &b);
+        R::str(d, &a, &b);
         if (version >= 1) {
-          rd_skip(d, 4);
-          rd_str(d, &a, &b);
+          R::skip(d, 4);
+          R::str(d, &a, &b);
         }
-        if (version >= 2) rd_skip(d, 8);
+        if (version >= 2) R::skip(d, 8);
         break;
       case 9:  // ReadOffsetFetchReq messages.go:1374-1411
-        rd_str(d, &a, &b);
+        R::str(d, &a, &b);
         break;
       case 10:  // ReadConsumerMetadataReq messages.go:1018-1039: no topics
-        rd_str(d, &a, &b);
-        if (version >= 1) rd_skip(d, 1);
+        R::str(d, &a, &b);
+        if (version >= 1) R::skip(d, 1);
         break;
       default:  // 3: ReadMetadataReq messages.go:493-522
         break;
     }
     int32_t n = 0;
-    if (kind != 10 && !rd_arraylen(d, &n)) ok = false;
+    if (kind != 10 && !arraylen(d, &n)) ok = false;
     start_topics(n);
     // Fixed partition entry sizes (0: variable or no partition array).
     const uint32_t esz = kind == 1 ? 16u + (version >= 5 ? 8u : 0u)
@@ -461,7 +507,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       topic();
       if (kind == 3 || d.err) continue;
       int32_t np;
-      if (!rd_arraylen(d, &np)) {
+      if (!arraylen(d, &np)) {
         ok = false;
         break;
       }
@@ -475,8 +521,8 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
         }
       } else if (kind == 0) {
         for (int32_t p = 0; p < np; ++p) {
-          rd_skip(d, 4);  // partition
-          const int32_t mss = rd_i32(d);
+          R::skip(d, 4);  // partition
+          const int32_t mss = static_cast<int32_t>(R::be(d, 4));
           if (d.err) break;
           if (read_message_set(d, mss, version, crc_tab, comp) == kMsErr) {
             ok = false;
@@ -485,12 +531,12 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
         }
       } else {  // 8
         for (int32_t p = 0; p < np && !d.err; ++p) {
-          rd_skip(d, 4 + 8 + (version == 1 ? 8 : 0));
-          rd_str(d, &a, &b);
+          R::skip(d, 4 + 8 + (version == 1 ? 8 : 0));
+          R::str(d, &a, &b);
         }
       }
     }
-    if (kind == 3 && version >= 4) rd_skip(d, 1);
+    if (kind == 3 && version >= 4) R::skip(d, 1);
     if (!ok || d.err) return L7M_VERDICT_PARSE_ERROR;
     if (kind == 10) {
       // ConsumerMetadataReq: GetTopics() is nil and ruleMatches -> true.

@@ -191,3 +191,38 @@ def test_lds_placement_variants_parity(gpu, budget):
     bad = np.nonzero(got != exp)[0]
     assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
     assert int(h.sum()) == len(offs)
+
+
+@pytest.mark.parametrize("n_fields", [1, 4, 8])
+def test_end_code_storage_and_header_jobs(gpu, n_fields):
+    """Programs with <= 4, 5-8 and > 8 value DFAs keep end codes in 4
+    registers, 8 registers or LDS columns (l7m_kernels.hip Codes<>); header
+    jobs skip names of unreferenced lengths, hash the rest, take the first
+    occurrence; presence-keyed rules go through the presence mask."""
+    rng = np.random.default_rng(7000 + n_fields)
+    names = [f"x-h{j}" for j in range(n_fields)]
+    rules = []
+    for i in range(60):
+        hs = []
+        for j in rng.choice(n_fields, size=min(n_fields, 1 + int(rng.integers(0, 3))), replace=False):
+            hs.append(f"{names[j]}: v{int(rng.integers(0, 4))}" if rng.random() < 0.7 else names[j])
+        rules.append(L.PortRuleHTTP(Path=f"/p{i % 7}/.*" if rng.random() < 0.8 else "",
+                                    Method=["GET", "POST", ""][i % 3], Headers=hs))
+    reqs = []
+    for _ in range(3000):
+        hs = []
+        for _k in range(int(rng.integers(0, 7))):
+            r = rng.random()
+            if r < 0.6:
+                hs.append((names[int(rng.integers(0, n_fields))], f"v{int(rng.integers(0, 5))}"))
+            elif r < 0.8:  # an unreferenced name of a referenced length
+                hs.append((f"y-h{int(rng.integers(0, 9))}", "v1"))
+            else:
+                hs.append(("user-agent", "curl/7.88"))
+        reqs.append(L.HTTPRequest(["GET", "POST", "PUT"][int(rng.integers(0, 3))],
+                                  f"/p{int(rng.integers(0, 9))}/{int(rng.integers(0, 100))}", "h", hs))
+    arena, offs = L.pack_http(reqs)
+    rs = L.RuleSet.compile_http(rules)
+    assert (rs.info.n_dfas <= 4) == (n_fields == 1) and (rs.info.n_dfas > 8) == (n_fields == 8)
+    v = _check(rules, arena, offs, hits=True)
+    assert (v >= 0).any() and (v == -1).any()
