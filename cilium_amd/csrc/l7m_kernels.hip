@@ -68,17 +68,32 @@ __device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, c
 
 // Walk `len` bytes at byte `pos` of the record through one packed DFA
 // (dfa_pack.h): per byte ONE dependent slot-table read.  The dead state is
-// absorbing, so the exit test runs once per 4 bytes.
+// absorbing, so the exit test runs once per 8-byte block.
 #define L7M_WALK_BYTES(STEP, DEAD)                                          \
   {                                                                         \
-    for (; k + 4 <= len; k += 4) {                                          \
+    for (; k + 8 <= len; k += 8) {  /* 8-byte blocks: half the loop */     \
+      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);    \
+      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3); \
+      const uint32_t b4 = src.byte(pos + k + 4), b5 = src.byte(pos + k + 5); \
+      const uint32_t b6 = src.byte(pos + k + 6), b7 = src.byte(pos + k + 7); \
+      STEP(b0)                                                              \
+      STEP(b1)                                                              \
+      STEP(b2)                                                              \
+      STEP(b3)                                                              \
+      STEP(b4)                                                              \
+      STEP(b5)                                                              \
+      STEP(b6)                                                              \
+      STEP(b7)                                                              \
+      if (DEAD) break;                                                      \
+    }                                                                       \
+    if (k + 4 <= len && !(DEAD)) {  /* then at most one 4-byte block */    \
       const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);    \
       const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3); \
       STEP(b0)                                                              \
       STEP(b1)                                                              \
       STEP(b2)                                                              \
       STEP(b3)                                                              \
-      if (DEAD) break;                                                      \
+      k += 4;                                                               \
     }                                                                       \
     if (!(DEAD))                                                            \
       for (; k < len; ++k) STEP(src.byte(pos + k))                          \
