@@ -95,8 +95,13 @@ __device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, c
       STEP(b3)                                                              \
       k += 4;                                                               \
     }                                                                       \
-    if (!(DEAD))                                                            \
-      for (; k < len; ++k) STEP(src.byte(pos + k))                          \
+    if (k < len && !(DEAD)) {  /* the last 1-3 bytes, no loop */           \
+      STEP(src.byte(pos + k))                                               \
+      if (k + 1 < len) {                                                    \
+        STEP(src.byte(pos + k + 1))                                         \
+        if (k + 2 < len) STEP(src.byte(pos + k + 2))                        \
+      }                                                                     \
+    }                                                                       \
   }
 
 // HBM slot table: e = T[base + b]; base = (e & 0xff) == b ? e >> 8 : 0.
