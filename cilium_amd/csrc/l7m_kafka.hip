@@ -92,14 +92,6 @@ __device__ __forceinline__ void rd_str(Rd& d, uint32_t* off, uint32_t* len) {
   d.pos += static_cast<uint32_t>(n);
 }
 
-// DecodeArrayLen (serialization.go:155-163): false = ErrInvalidArrayLen.
-__device__ __forceinline__ bool rd_arraylen(Rd& d, int32_t* n) {
-  const int32_t v = rd_i32(d);
-  if (v < 0 || v > kKafkaMaxParseBuf) return false;
-  *n = v;
-  return true;
-}
-
 // DecodeBytes (serialization.go:165-192), value discarded.
 __device__ __forceinline__ void rd_skip_bytes(Rd& d) {
   if (d.err) return;
