@@ -6,12 +6,15 @@
 //   1. the tile's byte window [off_first, end_last) is copied HBM -> the
 //      wave's LDS stage with coalesced 16-byte non-temporal loads (the arena is
 //      streamed exactly once; the tile is cut short so the window fits);
-//   2. every referenced field (method / path / authority / values of headers
-//      whose lower-cased name the header-name DFA recognises) is walked
-//      through its packed DFA groups (dfa_pack.h): one dependent 4-byte LDS
-//      read per input byte, tables copied to LDS once per workgroup;
-//   3. the end codes select precomputed candidate rule lists (L2-resident);
-//      the first rule (input order) whose other matchers hold is the verdict.
+//   2. walk phase: every referenced field (method / path / authority / values
+//      of headers whose lower-cased name a rule references) is walked through
+//      its packed DFA groups (dfa_pack.h) in one loop of walk jobs: one
+//      dependent 4-byte LDS read per input byte, tables copied to LDS once per
+//      workgroup;
+//   3. the next tile's bytes are requested;
+//   4. verification phase: the end codes select precomputed candidate rule
+//      lists (L2-resident); the first rule (input order) whose other
+//      matchers hold is the verdict.
 // A record that is not inside its tile window (non-contiguous offsets, a
 // record larger than the stage, malformed lengths) is evaluated by the same
 // code reading HBM directly.
