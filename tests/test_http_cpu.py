@@ -225,3 +225,23 @@ def test_compiler_table_only_lds_placement_matches_oracle():
     P = HttpProgram(rs.program())
     assert any(d["lds_table"] != 0xFFFFFFFF and d["lds_es"] == 0xFFFFFFFF for d in P.dfas)
     assert (P.eval(arena, offs) == HttpOracle(rules).eval(arena, offs)).all()
+
+
+@pytest.mark.parametrize("cfg,n_rules", [(2, 1000), (1, None), (5, 400)])
+def test_verification_masks_match_candidate_tables(cfg, n_rules):
+    """The header's cand_dfas / pres_fields masks (the kernel's uniform skips
+    in verification) name exactly the DFAs with candidate entries and the
+    fields with presence-keyed check records."""
+    rules = W.rules(cfg, n_rules=n_rules) if n_rules else W.rules(cfg)
+    P = HttpProgram(L.RuleSet.compile_http(rules).program())
+    h = P.h
+    cand = h["cand_dfas_lo"] | h["cand_dfas_hi"] << 32
+    pres = h["pres_fields_lo"] | h["pres_fields_hi"] << 32
+    for k in range(h["n_dfas"]):
+        d = P.dfas[k]
+        n_ct = d["nsets"] + d["npats"]
+        has = any(P.w[d["ct_off"] + 16 * i] for i in range(n_ct))
+        assert bool(cand >> k & 1) == has, k
+    for f, fd in enumerate(P.fields):
+        assert bool(pres >> f & 1) == (fd[3] > 0), f
+    assert cand != 0
