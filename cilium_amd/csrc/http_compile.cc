@@ -155,6 +155,8 @@ int translate_http_rule(const l7m_http_rule& r, std::vector<HeaderMatcher>* out,
 
 namespace {
 
+constexpr size_t kLitMinBytes = 16;  // shorter literal values are walked byte by byte
+
 CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const PolicyPlan& plan, const l7m_opts& opts) {
   CompileResult res;
   auto fail = [&](int st, const std::string& m) {
@@ -397,11 +399,12 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     const PackedDfa* d;
     uint32_t field;
     uint32_t npats;
+    const Group* grp;  // nullptr for the name DFA
   };
   std::vector<DfaOut> all;
   for (uint32_t f = 0; f < nf; ++f)
-    for (auto& g : groups[f]) all.push_back({&g.pk, f, static_cast<uint32_t>(g.pats.size())});
-  if (has_name) all.push_back({&name_dfa, kNone, nf - 3});
+    for (auto& g : groups[f]) all.push_back({&g.pk, f, static_cast<uint32_t>(g.pats.size()), &g});
+  if (has_name) all.push_back({&name_dfa, kNone, nf - 3, nullptr});
   const uint32_t ndt = static_cast<uint32_t>(all.size());
 
   std::vector<DfaDesc> dd(ndt);
@@ -423,6 +426,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     dd[k].nstates = d.nstates;
     dd[k].lds_table = dd[k].lds_es = dd[k].lds_latch = dd[k].lds_ct = dd[k].lds_mask = kNone;
     dd[k].lds_ctmask = kNone;
+    dd[k].lit_tab = kNone;
     total_states += d.nstates;
     for (size_t s = 0; s < d.sets.size(); ++s) {
       sets.push_back(push_list(d.sets[s]));
@@ -630,6 +634,30 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     dd[k].ct_off = take(16 * ct[k].size());
     dd[k].ctmask_off = take((ct[k].size() + 31) / 32);
   }
+  // Literal values of HBM-walked DFAs (program.h DfaDesc::lit_tab): once such
+  // a walk is latched on a literal pattern, the kernel compares the rest of
+  // the field with the literal directly (independent loads) instead of one
+  // dependent table read per byte.
+  std::vector<std::vector<uint32_t>> lit_words(ndt);
+  for (uint32_t k = 0; k < ndfa; ++k) {
+    if (dd[k].lds_table != kNone || !all[k].grp) continue;
+    const Group& g = *all[k].grp;
+    bool any = false;
+    for (uint32_t l = 0; l < g.pats.size(); ++l) {
+      const FieldPattern& fp = fpats[all[k].field][g.pats[l]];
+      any |= fp.kind == MatchKind::Value && fp.value.size() >= kLitMinBytes;
+    }
+    if (!any) continue;
+    dd[k].lit_tab = take(2ull * g.pats.size());
+    std::vector<uint32_t>& lw = lit_words[k];
+    lw.assign(2ull * g.pats.size(), kNone);
+    for (uint32_t l = 0; l < g.pats.size(); ++l) {
+      const FieldPattern& fp = fpats[all[k].field][g.pats[l]];
+      if (fp.kind != MatchKind::Value || fp.value.size() < kLitMinBytes) continue;
+      lw[2 * l] = take((fp.value.size() + 3) / 4);
+      lw[2 * l + 1] = static_cast<uint32_t>(fp.value.size());
+    }
+  }
   w = (w + 63) & ~uint64_t(63);  // 256-byte aligned image
   h.lds_image_off = take(img);
   h.lds_image_words = static_cast<uint32_t>(img);
@@ -667,6 +695,15 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       }
     }
     if (!ce.empty()) std::memcpy(P + dd[k].ct_off, ce.data(), ce.size() * sizeof(CandEntry));
+    if (dd[k].lit_tab != kNone) {
+      const std::vector<uint32_t>& lw = lit_words[k];
+      std::memcpy(P + dd[k].lit_tab, lw.data(), lw.size() * 4);
+      for (uint32_t l = 0; l < all[k].npats; ++l)
+        if (lw[2 * l] != kNone) {
+          const std::string& v = fpats[all[k].field][all[k].grp->pats[l]].value;
+          std::memcpy(P + lw[2 * l], v.data(), v.size());
+        }
+    }
     if (dd[k].lds_table != kNone) {
       // the LDS copy names rows by image word index (program.h kLdsRowShift),
       // with the target state's end code when it fits 8 bits

@@ -197,6 +197,9 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
     HttpHeader h;
     std::memcpy(&h, rs->program.data(), sizeof h);
     if (http_stage_bytes(h) == 0) return L7M_ETOOBIG;
+    const DfaDesc* dd = reinterpret_cast<const DfaDesc*>(rs->program.data() + h.off_dfas);
+    for (uint32_t k = 0; k < h.n_dfas; ++k)
+      if (dd[k].lit_tab != kNone) flags |= kLaunchLiterals;
     e = launch_http(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
                     n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
                     stream, cus, flags);

@@ -33,6 +33,10 @@ inline hipError_t set_lds_attr_once(const void* fn, uint32_t bytes) {
 // the stage the LDS leaves after the rule tables (0: the tables do not fit).
 size_t http_lds_bytes(const HttpHeader& h, uint32_t stage);
 uint32_t http_stage_bytes(const HttpHeader& h);
+// Internal launch flag (beside the public L7M_FLAG_* bits): the program has
+// literal tables (DfaDesc::lit_tab), so the kernel instantiation that uses
+// them is launched.
+constexpr uint32_t kLaunchLiterals = 1u << 29;  // L7M_FLAG_DIAG_* use bits 30, 31
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags);

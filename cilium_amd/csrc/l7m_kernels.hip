@@ -108,7 +108,7 @@ __device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, c
   }
 
 // HBM slot table: e = T[base + b]; base = (e & 0xff) == b ? e >> 8 : 0.
-template <class Src>
+template <bool kLit, class Src>
 __device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
                                              const DfaDesc& dd, const Src& src, uint32_t pos, uint32_t len) {
   const uint32_t* __restrict__ T = prog + dd.table_off;
@@ -124,7 +124,54 @@ __device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, c
     base = (e_ & 0xffu) == b_ ? (e_ >> 8) : 0u;            \
   }
   uint32_t k = 0;
-  if (base) L7M_WALK_BYTES(L7M_STEP, !base)
+  if (!kLit || dd.lit_tab == kNone) {
+    if (base) L7M_WALK_BYTES(L7M_STEP, !base)
+    return end_code<false>(img, prog, dd, base, last);
+  }
+  // DFA with literal values (program.h lit_tab): 8-byte blocks until the walk
+  // is latched on one pattern; a latched literal is then compared directly.
+  bool lit_stop = false;
+  if (base) {
+    for (; k + 8 <= len; k += 8) {
+      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
+      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
+      const uint32_t b4 = src.byte(pos + k + 4), b5 = src.byte(pos + k + 5);
+      const uint32_t b6 = src.byte(pos + k + 6), b7 = src.byte(pos + k + 7);
+      L7M_STEP(b0)
+      L7M_STEP(b1)
+      L7M_STEP(b2)
+      L7M_STEP(b3)
+      L7M_STEP(b4)
+      L7M_STEP(b5)
+      L7M_STEP(b6)
+      L7M_STEP(b7)
+      if (!base) break;
+      if (base >= region) {
+        k += 8;
+        lit_stop = true;
+        break;
+      }
+    }
+    if (base && !lit_stop) L7M_WALK_BYTES(L7M_STEP, !base)
+  }
+  if (lit_stop) {
+    const uint32_t p = last == kNone ? dd.start_latch : prog[dd.latch_off + last];
+    const uint32_t lo = prog[dd.lit_tab + 2 * p], ll = prog[dd.lit_tab + 2 * p + 1];
+    if (lo != kNone) {
+      // bytes [0, k) followed the literal (the walk is latched on it): the
+      // field matches iff it has the literal's length and the rest is equal
+      if (ll != len) return 0;
+      const uint8_t* L = reinterpret_cast<const uint8_t*>(prog + lo);
+      uint32_t x = 0, i = k;
+      for (; !x && i + 8 <= len; i += 8) {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) x |= src.byte(pos + i + j) ^ L[i + j];
+      }
+      for (; !x && i < len; ++i) x |= src.byte(pos + i) ^ L[i];
+      return x ? 0u : (kLatchedBit | p);
+    }
+    L7M_WALK_BYTES(L7M_STEP, !base)  // latched on a non-literal pattern: walk on
+  }
 #undef L7M_STEP
   return end_code<false>(img, prog, dd, base, last);
 }
@@ -272,11 +319,11 @@ struct Ctx {
   const Span* remotes;         // HBM
 };
 
-template <class Src>
+template <bool kLit, class Src>
 __device__ __forceinline__ uint32_t walk_dfa(const Ctx& c, uint32_t d, const Src& src, uint32_t pos, uint32_t len) {
   const DfaDesc& dd = c.dds[d];
   if (dd.lds_table != kNone) return walk_lds(c.img, c.prog, dd, src, pos, len);
-  return walk_hbm(c.img, c.prog, dd, src, pos, len);
+  return walk_hbm<kLit>(c.img, c.prog, dd, src, pos, len);
 }
 
 // Field id of the header name at byte `pos` (length len) of the record, via
@@ -384,7 +431,7 @@ constexpr int32_t kNeedVerify = INT32_MIN;
 // when it is decided without rules, else kNeedVerify with `o` filled in.
 // kAblate (diagnostic builds selected by L7M_FLAG_DIAG_*; verdicts invalid):
 // 1 = stop after the DFA walks, 2 = stop after record validation.
-template <int kReg, int kAblate, class Src>
+template <int kReg, int kAblate, bool kLit, class Src>
 __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit,
                                              WalkOut<kReg>& o PROF_PARAM) {
 #ifdef L7M_PROF
@@ -482,7 +529,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         if (h.lds_name_tab != kNone) {
           f = name_field_of(c, h, src, hp, nl);
         } else {
-          const uint32_t code = walk_dfa(c, h.n_dfas, src, hp, nl);
+          const uint32_t code = walk_dfa<false>(c, h.n_dfas, src, hp, nl);
           if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
           else if (code) f = c.name_field[code];
         }
@@ -498,7 +545,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
       const FieldDesc& fd = c.fields[f];
       for (uint32_t k = 0; k < fd.ndfa; ++k) {
         const uint32_t d = fd.dfa_first + k;
-        const uint32_t code = walk_dfa(c, d, src, p, len);
+        const uint32_t code = walk_dfa<kLit>(c, d, src, p, len);
         codes.set(d, code);
         touch(d, code);
       }
@@ -644,7 +691,10 @@ __device__ __forceinline__ void wave_sync() {
 // end (small rule sets), or wave-aggregated global atomics.
 enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
 
-template <int kHits, int kReg, int kAblate>
+// kLit: the program has literal tables (DfaDesc::lit_tab) for HBM-walked
+// DFAs; a separate instantiation, so programs without them keep the leaner
+// walk code.
+template <int kHits, int kReg, int kAblate, bool kLit>
 __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,
                                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                            const uint64_t* __restrict__ offs, uint64_t n,
@@ -759,14 +809,14 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
         const LdsSrc s{reinterpret_cast<const uint32_t*>(stg + (o - base))};
         const uint32_t w0 = s.word(0);
         if (((static_cast<uint64_t>(w0) + 3) & ~3ull) <= onext - o) {
-          v = eval_walk<kReg, kAblate>(c, h, s, onext - o, wo PROF_ARG);
+          v = eval_walk<kReg, kAblate, kLit>(c, h, s, onext - o, wo PROF_ARG);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: read HBM directly
         const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
         const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-        v = inb ? eval_walk<kReg, kAblate>(c, h, s, arena_bytes - o, wo PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
+        v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
       }
     }
     // The next tile's bytes are requested only now, after the walks: they
@@ -836,16 +886,16 @@ uint32_t http_stage_bytes(const HttpHeader& h) {
   return static_cast<uint32_t>(s > kMaxStage ? kMaxStage : s);
 }
 
-template <int kHits, int kReg, int kAblate = 0>
+template <int kHits, int kReg, int kAblate = 0, bool kLit = false>
 static hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, uint32_t stage) {
   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU); set per device
   // and instantiation, thread-safely (l7m_device.h)
-  const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate>),
+  const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate, kLit>),
                                          kLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
+  hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate, kLit>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
                      offs, n, verdicts, hits, stage);
   return hipGetLastError();
 }
@@ -871,8 +921,13 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   }
   const int mode = !hits ? kNoHits : (h.n_rules + 2 <= kMaxLdsCounters ? kLdsHits : kGlobalHits);
   // end codes in 4 or 8 registers, or in LDS columns
-#define L7M_LAUNCH(M, R) \
-  return launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage)
+  const bool lit = (flags & kLaunchLiterals) != 0;
+#define L7M_LAUNCH(M, R)                                                                                         \
+  {                                                                                                              \
+    if (lit) return launch_one<M, R, 0, true>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts,   \
+                                              hits, stage);                                                      \
+    return launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);       \
+  }
 #define L7M_LAUNCH_R(M)                 \
   {                                     \
     if (h.n_dfas <= 4) L7M_LAUNCH(M, 4); \

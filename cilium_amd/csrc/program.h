@@ -68,7 +68,9 @@ struct DfaDesc {
   uint32_t lds_ctmask;   // LDS image word offset of a bitmask: ct entry i has candidates, or kNone
   uint32_t ctmask_off;   // program: the same bitmask (always)
   uint32_t start_es8;    // lds_es == kLdsEsInEntry: the start state's end code (es8)
-  uint32_t pad[3];
+  uint32_t lit_tab;      // program: u32 pairs per local pattern {word offset, length} of its
+                         // literal value (kNone: not a literal), or kNone (HBM-walked DFAs only)
+  uint32_t pad[2];
 };
 static_assert(sizeof(DfaDesc) == 96, "dfa desc is 24 words");
 
