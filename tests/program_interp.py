@@ -23,7 +23,7 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi "
               "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
-              "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8").split()
+              "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab").split()
 ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 
 

@@ -53,3 +53,29 @@ def test_many_dfa_groups_are_rejected_at_compile_time():
         L.RuleSet.compile_http(rules, dialect=L.DIALECT_RE2_SEARCH)
     assert e.value.code == L.L7M_ETOOBIG
     assert "fixed LDS" in str(e.value)
+
+
+def test_literal_tables_of_hbm_walked_dfas():
+    """Config 5's x-blob literals (1 KiB header values) sit in HBM-walked
+    automata: their DFAs carry literal tables (program.h DfaDesc::lit_tab)
+    whose entries hold exactly the rules' values, so the kernel can compare a
+    latched literal directly (l7m_kernels.hip walk_hbm)."""
+    import numpy as np
+    from program_interp import HttpProgram, KNONE
+    rules = W.rules(5, n_rules=2000)
+    blobs = {h.split(": ", 1)[1] for r in rules for h in r.Headers if h.lower().startswith("x-blob")}
+    assert blobs
+    rs = L.RuleSet.compile_http(rules)
+    prog = rs.program()
+    P = HttpProgram(prog)
+    raw = prog.astype(np.uint32).tobytes()
+    found = set()
+    for d in P.dfas[:P.h["n_dfas"]]:
+        if d["lit_tab"] == KNONE:
+            continue
+        assert d["lds_table"] == KNONE  # only HBM-walked automata carry them
+        for p in range(d["npats"]):
+            off, n = P.w[d["lit_tab"] + 2 * p], P.w[d["lit_tab"] + 2 * p + 1]
+            if off != KNONE:
+                found.add(raw[4 * off: 4 * off + n].decode())
+    assert found == {b for b in blobs if len(b) >= 16}
