@@ -429,4 +429,18 @@ uint64_t l7g_requests(int config, uint64_t seed, uint32_t n_rules, uint64_t star
   return total;
 }
 
+// Bytes of records [start, start + count) summed per block of `block`
+// records (sizes only, nothing written): the input of byte-balanced shard
+// bounds over a batch too large to generate on one rank (cilium_amd/dist.py).
+void l7g_block_bytes(int config, uint64_t seed, uint32_t n_rules, uint64_t start, uint64_t count, uint64_t block,
+                     uint64_t* out, int threads) {
+  const uint64_t nb = (count + block - 1) / block;
+  parallel(nb, threads, [&](uint64_t a, uint64_t b) {
+    for (uint64_t j = a; j < b; ++j) {
+      const uint64_t lo = start + j * block, n = std::min(block, count - j * block);
+      out[j] = l7g_requests(config, seed, n_rules, lo, n, nullptr, 0, nullptr, 1);
+    }
+  });
+}
+
 }  // extern "C"

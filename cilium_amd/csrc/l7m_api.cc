@@ -225,6 +225,8 @@ constexpr int kMaxDevices = 64;
 
 struct EvalCtx {
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // second stream of the chunked pipeline (lazily created)
+  hipEvent_t ev = nullptr, ev2 = nullptr;
   void *arena = nullptr, *offs = nullptr, *verd = nullptr, *hits = nullptr, *ids = nullptr;
   size_t cap_arena = 0, cap_offs = 0, cap_verd = 0, cap_hits = 0, cap_ids = 0;
   std::vector<uint64_t> hhost;
@@ -279,6 +281,67 @@ EvalCtx* acquire_ctx(int dev) {
 void release_ctx(int dev, EvalCtx* c) {
   std::lock_guard<std::mutex> g(g_pools[dev].mu);
   g_pools[dev].free.push_back(c);
+}
+
+// Large host batches are pipelined: the arena is cut at record boundaries
+// into chunks of ~kPipeChunkBytes, and chunk k's H2D copy, kernel and D2H of
+// verdicts are enqueued on stream k & 1, so chunk k+1's copy overlaps chunk
+// k's kernel (SURVEY.md §8(d) end-to-end).  The device arena keeps the host
+// layout (offsets stay valid); the kernels read only their own chunk's
+// records.  Needs ascending offsets (what every packer produces); other
+// batches take the one-shot path.  Pass pinned memory (l7m_alloc_pinned) for
+// DMA-rate copies.
+constexpr size_t kPipeChunkBytes = size_t(64) << 20;
+
+bool ascending(const uint64_t* offs, size_t n, size_t arena_bytes) {
+  for (size_t i = 1; i < n; ++i)
+    if (offs[i] < offs[i - 1]) return false;
+  return n == 0 || offs[n - 1] < arena_bytes;
+}
+
+int eval_pipelined(EvalCtx* c, const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
+                   const uint64_t* offsets, size_t n, const uint32_t* ids, int32_t* verdicts, bool hits,
+                   size_t abytes, size_t nctr, uint32_t flags) {
+  if (!c->stream2 && hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) return L7M_EDEVICE;
+  if (!c->ev && hipEventCreateWithFlags(&c->ev, hipEventDisableTiming) != hipSuccess) return L7M_EDEVICE;
+  if (!c->ev2 && hipEventCreateWithFlags(&c->ev2, hipEventDisableTiming) != hipSuccess) return L7M_EDEVICE;
+  const hipStream_t s0 = c->stream, s1 = c->stream2;
+  auto* da = static_cast<uint8_t*>(c->arena);
+  auto* doffs = static_cast<uint64_t*>(c->offs);
+  auto* dverd = static_cast<int32_t*>(c->verd);
+  auto* dids = static_cast<uint32_t*>(c->ids);
+  bool ok = hipMemsetAsync(da + arena_bytes, 0, abytes - arena_bytes, s0) == hipSuccess &&
+            (!hits || hipMemsetAsync(c->hits, 0, nctr * 8, s0) == hipSuccess) &&
+            hipEventRecord(c->ev, s0) == hipSuccess && hipStreamWaitEvent(s1, c->ev, 0) == hipSuccess;
+  int rc = ok ? L7M_OK : L7M_EDEVICE;
+  size_t lo = 0;
+  for (int k = 0; rc == L7M_OK && lo < n; ++k) {
+    const uint64_t a = k == 0 ? 0 : offsets[lo];
+    // first record starting at or past a + chunk: the chunk ends there
+    size_t hi = static_cast<size_t>(std::lower_bound(offsets + lo, offsets + n, a + kPipeChunkBytes) - offsets);
+    if (hi == lo) hi = lo + 1;
+    const uint64_t b = hi < n ? offsets[hi] : arena_bytes;
+    const hipStream_t st = (k & 1) ? s1 : s0;
+    ok = hipMemcpyAsync(da + a, arena + a, b - a, hipMemcpyHostToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(doffs + lo, offsets + lo, (hi - lo) * 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+         (!ids || hipMemcpyAsync(dids + lo, ids + lo, (hi - lo) * 4, hipMemcpyHostToDevice, st) == hipSuccess);
+    if (!ok) rc = L7M_EDEVICE;
+    if (rc == L7M_OK)
+      rc = launch(rs, da, arena_bytes, doffs + lo, hi - lo, dverd + lo, hits ? c->hits : nullptr, st, flags,
+                  ids ? dids + lo : nullptr);
+    if (rc == L7M_OK &&
+        hipMemcpyAsync(verdicts + lo, dverd + lo, (hi - lo) * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = L7M_EDEVICE;
+    lo = hi;
+  }
+  // join: stream 0 waits for stream 1, then the counters come back
+  if (hipEventRecord(c->ev2, s1) != hipSuccess || hipStreamWaitEvent(s0, c->ev2, 0) != hipSuccess) rc = L7M_EDEVICE;
+  if (rc == L7M_OK && hits &&
+      hipMemcpyAsync(c->hhost.data(), c->hits, nctr * 8, hipMemcpyDeviceToHost, s0) != hipSuccess)
+    rc = L7M_EDEVICE;
+  if (hipStreamSynchronize(s0) != hipSuccess && rc == L7M_OK) rc = L7M_EDEVICE;
+  if (hipStreamSynchronize(s1) != hipSuccess && rc == L7M_OK) rc = L7M_EDEVICE;
+  return rc;
 }
 
 }  // namespace
@@ -511,7 +574,11 @@ int l7m_eval_ids(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes
   EvalCtx* c = acquire_ctx(dev);
   if (!c) return L7M_EDEVICE;
   int rc = c->reserve(abytes, n, nctr, ids != nullptr);
-  if (rc == L7M_OK) {
+  if (rc == L7M_OK && arena_bytes >= 2 * kPipeChunkBytes && ascending(offsets, n, arena_bytes)) {
+    rc = eval_pipelined(c, rs, arena, arena_bytes, offsets, n, ids, verdicts, hits != nullptr, abytes, nctr, flags);
+    if (rc == L7M_OK && hits)
+      for (size_t i = 0; i < nctr; ++i) hits[i] += c->hhost[i];
+  } else if (rc == L7M_OK) {
     const hipStream_t st = c->stream;
     bool ok = hipMemsetAsync(static_cast<uint8_t*>(c->arena) + arena_bytes, 0, abytes - arena_bytes, st) == hipSuccess &&
               hipMemcpyAsync(c->arena, arena, arena_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&

@@ -8,13 +8,20 @@
 // per request would cost more than the verdict, so the batcher keeps that
 // per-request, blocking call shape while many callers' requests share one
 // l7m_eval: a caller appends its record to the batch being filled and waits;
-// a flusher thread evaluates the batch when it holds max_batch requests or
-// its first request has waited max_delay_us, while the next batch fills.
+// a flusher evaluates the batch when it holds max_batch requests or its first
+// request has waited max_delay_us, while the next batch fills.
+//
+// Pipelining: `in_flight` flusher threads (default 2) each take the next
+// ready batch, so batch k+1's H2D copy runs while batch k's kernel and D2H
+// run (l7m_eval is reentrant: every call has its own stream and device
+// buffers).  Batches live in pinned host memory (recycled, never freed while
+// the batcher lives), so the copies are DMA transfers, not staged.
 // l7m_batcher_set_ruleset is the policy update (Redirect.updateRules,
 // pkg/proxy/redirect.go:68-74): batches flushed afterwards use the new rules.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstddef>
 #include <condition_variable>
 #include <cstring>
 #include <memory>
@@ -28,57 +35,109 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+// Growable pinned host buffer (hipHostMalloc); grows by doubling.
+template <class T>
+struct PinnedVec {
+  T* p = nullptr;
+  size_t n = 0, cap = 0;
+  PinnedVec() = default;
+  PinnedVec(const PinnedVec&) = delete;
+  PinnedVec& operator=(const PinnedVec&) = delete;
+  ~PinnedVec() {
+    if (p) (void)hipHostFree(p);
+  }
+  bool reserve(size_t want) {
+    if (want <= cap) return true;
+    size_t c = cap ? cap : 1024;
+    while (c < want) c *= 2;
+    void* q = nullptr;
+    if (hipHostMalloc(&q, c * sizeof(T), hipHostMallocDefault) != hipSuccess) return false;
+    if (n) std::memcpy(q, p, n * sizeof(T));
+    if (p) (void)hipHostFree(p);
+    p = static_cast<T*>(q);
+    cap = c;
+    return true;
+  }
+};
+
 struct Batch {
-  std::vector<uint8_t> arena;
-  std::vector<uint64_t> offs;
-  std::vector<uint32_t> ids;  // source identities (Kafka rule sets)
-  std::vector<int32_t> verd;
+  PinnedVec<uint8_t> arena;
+  PinnedVec<uint64_t> offs;
+  PinnedVec<uint32_t> ids;  // source identities (Kafka rule sets)
+  PinnedVec<int32_t> verd;
   Clock::time_point first;
   bool done = false;
   int rc = L7M_OK;
+  uint32_t waiters = 0;  // callers that have not read their verdict yet
+  void reset() {
+    arena.n = offs.n = ids.n = verd.n = 0;
+    done = false;
+    rc = L7M_OK;
+    waiters = 0;
+  }
 };
 
 }  // namespace
 
 struct l7m_batcher {
   std::mutex mu;
-  std::condition_variable cv_flush, cv_done;
+  std::condition_variable cv_flush, cv_done, cv_idle;
   l7m_ruleset* rs = nullptr;
   uint32_t max_batch = 65536;
   uint32_t max_delay_us = 200;
+  uint32_t in_flight = 2;
   int device = 0;
-  std::shared_ptr<Batch> cur = std::make_shared<Batch>();
+  Batch* cur = nullptr;
+  std::vector<Batch*> pool;     // recycled batches (pinned buffers kept)
+  std::vector<Batch*> all;      // every batch ever made (freed at destroy)
   bool stop = false;
+  uint32_t callers = 0;         // threads inside eval()
   uint64_t batches = 0, requests = 0;
-  std::thread flusher;
+  std::vector<std::thread> flushers;
+
+  Batch* fresh() {  // under mu
+    Batch* b;
+    if (!pool.empty()) {
+      b = pool.back();
+      pool.pop_back();
+    } else {
+      b = new Batch();
+      all.push_back(b);
+    }
+    b->reset();
+    return b;
+  }
 
   void run() {
     (void)hipSetDevice(device);
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      while (!stop && cur->offs.empty()) cv_flush.wait(lk);
-      if (cur->offs.empty() && stop) return;
+      while (!stop && cur->offs.n == 0) cv_flush.wait(lk);
+      if (cur->offs.n == 0 && stop) return;
       // full, or the first request has waited long enough (or shutting down)
-      const auto deadline = cur->first + std::chrono::microseconds(max_delay_us);
-      while (!stop && cur->offs.size() < max_batch && Clock::now() < deadline) cv_flush.wait_until(lk, deadline);
-      std::shared_ptr<Batch> b = cur;
-      cur = std::make_shared<Batch>();
+      Batch* const b = cur;
+      const auto deadline = b->first + std::chrono::microseconds(max_delay_us);
+      while (!stop && cur == b && b->offs.n < max_batch && Clock::now() < deadline) cv_flush.wait_until(lk, deadline);
+      if (cur != b) continue;  // another flusher took it
+      cur = fresh();
       l7m_ruleset* r = rs;
       l7m_retain(r);
       ++batches;
-      requests += b->offs.size();
+      requests += b->offs.n;
       lk.unlock();
-      b->verd.resize(b->offs.size());
-      b->arena.resize(b->arena.size() + 64, 0);  // tail padding for aligned loads
-      l7m_ruleset_info info;
-      l7m_ruleset_get_info(r, &info);
-      const int rc = l7m_eval_ids(r, b->arena.data(), b->arena.size() - 64, b->offs.data(), b->offs.size(),
-                                  info.proto == L7M_PROTO_KAFKA ? b->ids.data() : nullptr, b->verd.data(), nullptr,
-                                  0);
+      cv_flush.notify_one();  // a second flusher may start on the next batch
+      int rc = b->verd.reserve(b->offs.n) ? L7M_OK : L7M_ENOMEM;
+      if (rc == L7M_OK) {
+        l7m_ruleset_info info;
+        l7m_ruleset_get_info(r, &info);
+        rc = l7m_eval_ids(r, b->arena.p, b->arena.n, b->offs.p, b->offs.n,
+                          info.proto == L7M_PROTO_KAFKA ? b->ids.p : nullptr, b->verd.p, nullptr, 0);
+      }
       l7m_release(r);
       lk.lock();
       b->rc = rc;
       b->done = true;
+      if (b->waiters == 0) pool.push_back(b);
       cv_done.notify_all();
     }
   }
@@ -86,19 +145,28 @@ struct l7m_batcher {
   int eval(const uint8_t* rec, size_t len, uint32_t src_identity, int32_t* verdict) {
     std::unique_lock<std::mutex> lk(mu);
     if (stop) return L7M_EINVAL;
-    std::shared_ptr<Batch> b = cur;
-    const size_t idx = b->offs.size();
+    Batch* b = cur;
+    const size_t idx = b->offs.n;
+    const size_t off = b->arena.n, padded = (len + 3) & ~size_t(3);
+    // + 64 bytes of zero tail for the kernels' aligned loads (l7m_eval pads its copy too)
+    if (!b->arena.reserve(off + padded + 64) || !b->offs.reserve(idx + 1) || !b->ids.reserve(idx + 1))
+      return L7M_ENOMEM;
+    ++callers;
     if (idx == 0) b->first = Clock::now();
-    const size_t off = b->arena.size();
-    b->offs.push_back(off);
-    b->ids.push_back(src_identity);
-    b->arena.resize(off + ((len + 3) & ~size_t(3)), 0);
-    if (len) std::memcpy(b->arena.data() + off, rec, len);
-    if (idx == 0 || b->offs.size() >= max_batch) cv_flush.notify_one();
+    b->offs.p[idx] = off;
+    b->ids.p[idx] = src_identity;
+    if (len) std::memcpy(b->arena.p + off, rec, len);
+    std::memset(b->arena.p + off + len, 0, padded - len);
+    b->arena.n = off + padded;
+    b->offs.n = idx + 1;
+    ++b->waiters;
+    if (idx == 0 || b->offs.n >= max_batch) cv_flush.notify_one();
     cv_done.wait(lk, [&] { return b->done; });
-    if (b->rc != L7M_OK) return b->rc;
-    *verdict = b->verd[idx];
-    return L7M_OK;
+    const int rc = b->rc;
+    if (rc == L7M_OK) *verdict = b->verd.p[idx];
+    if (--b->waiters == 0) pool.push_back(b);  // the last reader recycles it
+    if (--callers == 0) cv_idle.notify_all();
+    return rc;
   }
 };
 
@@ -114,11 +182,14 @@ int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batche
     std::memcpy(&o, opts, k);
     if (o.max_batch) b->max_batch = o.max_batch;
     if (o.max_delay_us) b->max_delay_us = o.max_delay_us;
+    if (k >= offsetof(l7m_batcher_opts, in_flight) + sizeof o.in_flight && o.in_flight)
+      b->in_flight = o.in_flight > 8 ? 8 : o.in_flight;
     b->device = o.device;
   }
+  b->cur = b->fresh();
   l7m_retain(rs);
   b->rs = rs;
-  b->flusher = std::thread([b] { b->run(); });
+  for (uint32_t i = 0; i < b->in_flight; ++i) b->flushers.emplace_back([b] { b->run(); });
   *out = b;
   return L7M_OK;
 }
@@ -164,6 +235,9 @@ int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests) {
   return L7M_OK;
 }
 
+// Safe with calls in flight: pending batches are still evaluated, new calls
+// get L7M_EINVAL, and the batcher is freed only after every caller inside
+// l7m_batcher_eval* has read its verdict and left.
 void l7m_batcher_destroy(l7m_batcher* b) {
   if (!b) return;
   {
@@ -171,8 +245,14 @@ void l7m_batcher_destroy(l7m_batcher* b) {
     b->stop = true;
   }
   b->cv_flush.notify_all();
-  if (b->flusher.joinable()) b->flusher.join();
+  for (auto& t : b->flushers)
+    if (t.joinable()) t.join();
+  {
+    std::unique_lock<std::mutex> lk(b->mu);
+    b->cv_idle.wait(lk, [&] { return b->callers == 0; });
+  }
   l7m_release(b->rs);
+  for (Batch* x : b->all) delete x;
   delete b;
 }
 

@@ -142,7 +142,7 @@ class _NetworkPolicy(ctypes.Structure):
 
 class _BatcherOpts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("max_batch", ctypes.c_uint32),
-                ("max_delay_us", ctypes.c_uint32), ("device", ctypes.c_int32)]
+                ("max_delay_us", ctypes.c_uint32), ("device", ctypes.c_int32), ("in_flight", ctypes.c_uint32)]
 
 
 class _ProxyStats(ctypes.Structure):
@@ -622,9 +622,10 @@ class Batcher:
     """l7m_batcher: blocking per-request verdicts shared in GPU batches (the
     canAccess / decodeHeaders call shape, see include/l7match.h)."""
 
-    def __init__(self, ruleset: "RuleSet", max_batch: int = 0, max_delay_us: int = 0, device: int = 0):
+    def __init__(self, ruleset: "RuleSet", max_batch: int = 0, max_delay_us: int = 0, device: int = 0,
+                 in_flight: int = 0):
         self.ruleset = ruleset
-        opts = _BatcherOpts(ctypes.sizeof(_BatcherOpts), max_batch, max_delay_us, device)
+        opts = _BatcherOpts(ctypes.sizeof(_BatcherOpts), max_batch, max_delay_us, device, in_flight)
         h = ctypes.c_void_p()
         rc = _lib.l7m_batcher_create(ruleset.handle, ctypes.byref(opts), ctypes.byref(h))
         if rc != L7M_OK:

@@ -36,6 +36,9 @@ def _load():
                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                ctypes.c_int]
     g.l7g_requests.restype = ctypes.c_uint64
+    g.l7g_block_bytes.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+    g.l7g_block_bytes.restype = None
     return g
 
 
@@ -75,6 +78,19 @@ def requests(config: int, start: int, count: int, seed: int = None, n_rules: int
                              offs.ctypes.data, threads)
     assert used == size
     return arena[: size + 64] if out_arena is None else arena, offs
+
+
+def block_bytes(config: int, start: int, count: int, block: int, seed: int = None, n_rules: int = None,
+                threads: int = 8) -> np.ndarray:
+    """Record bytes of requests [start, start+count) summed per `block` records
+    (sizes only): the input of byte-balanced shard bounds (dist.py)."""
+    c = CONFIGS[config]
+    seed = c["seed"] if seed is None else seed
+    n_rules = c["n_rules"] if n_rules is None else n_rules
+    out = np.zeros((count + block - 1) // block, dtype=np.uint64)
+    if count:
+        _gen.l7g_block_bytes(config, seed, n_rules, start, count, block, out.ctypes.data, threads)
+    return out
 
 
 def mixed_parts(config: int = 4):

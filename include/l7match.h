@@ -347,7 +347,12 @@ int l7m_eval_device_ids(const l7m_ruleset* rs, const void* d_arena, size_t arena
  * connection's goroutine / worker thread.  l7m_batcher keeps that blocking
  * per-request call: any number of threads call l7m_batcher_eval; their
  * records share one l7m_eval, flushed when max_batch requests are pending or
- * the first has waited max_delay_us, while the next batch fills.
+ * the first has waited max_delay_us, while the next batch fills.  Up to
+ * in_flight batches are evaluated at once (batch k+1's H2D copy overlaps
+ * batch k's kernel); batches live in pinned host memory.  Destroying a
+ * batcher with calls in flight is safe: pending batches are still decided,
+ * later calls get L7M_EINVAL, and the memory is freed after the last caller
+ * has returned.
  * l7m_batcher_set_ruleset swaps the rules for later batches (the
  * Redirect.updateRules policy update, pkg/proxy/redirect.go:68-74). */
 typedef struct l7m_batcher l7m_batcher;
@@ -356,6 +361,7 @@ typedef struct {
   uint32_t max_batch;    /* requests per evaluation (0 = 65536)             */
   uint32_t max_delay_us; /* longest wait of a batch's first request (0 = 200) */
   int32_t device;        /* HIP device the batches run on                   */
+  uint32_t in_flight;    /* batches evaluated concurrently (0 = 2, max 8)   */
 } l7m_batcher_opts;
 int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batcher** out);
 int l7m_batcher_set_ruleset(l7m_batcher* b, l7m_ruleset* rs);

@@ -33,11 +33,18 @@
 //                          DEFLATE by zlib), snappy (github.com/golang/snappy decode.go,
 //                          proto/snappy.go), decoded sets read recursively
 //   MatchesRule            pkg/kafka/policy.go:27-225
+// Regex engines: std::regex (the reference engine, default) or the
+// Thompson-NFA / Pike-VM simulator of nfa.h (engine 1, the long-input oracle
+// of SURVEY.md §8(c): the same membership, linear time, no recursion; pinned
+// against std::regex by tests/cpp/fuzz_nfa.cc).  With engine 1 each pattern is
+// still compiled by std::regex too, so NACK parity (L7M_EINVAL_REGEX) is the
+// reference's.
 // Verdict encoding matches include/l7match.h (-1 deny, i >= 0 deciding rule).
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <regex>
 #include <set>
 #include <unordered_map>
@@ -49,6 +56,7 @@
 #include <zlib.h>
 
 #include "../include/l7match.h"
+#include "nfa.h"
 
 namespace {
 
@@ -70,7 +78,17 @@ struct HeaderData {
   int kind;  // 0 regex, 1 value, 2 present
   std::string value;
   std::regex re;
+  std::shared_ptr<const nfa::Prog> nfa;  // engine 1
 };
+
+// regex_match / regex_search of a kind-0 matcher with the selected engine
+bool regex_ok(const HeaderData& hd, const std::string& v, bool search) {
+  if (hd.nfa) {
+    thread_local nfa::Runner run;
+    return run.run(*hd.nfa, reinterpret_cast<const uint8_t*>(v.data()), v.size(), search);
+  }
+  return search ? std::regex_search(v, hd.re) : std::regex_match(v, hd.re);
+}
 struct HttpOracle {
   bool search = false;  // L7M_DIALECT_RE2_SEARCH
   std::vector<std::vector<HeaderData>> rules;
@@ -149,7 +167,7 @@ int32_t eval_http_one(const HttpOracle& o, const HttpReq& q) {
           break;
         }
       if (!v) { all = false; break; }
-      if (hd.kind == 0 && !(o.search ? std::regex_search(*v, hd.re) : std::regex_match(*v, hd.re))) {
+      if (hd.kind == 0 && !regex_ok(hd, *v, o.search)) {
         all = false;
         break;
       }
@@ -163,7 +181,7 @@ int32_t eval_http_one(const HttpOracle& o, const HttpReq& q) {
 // ============================================================= Kafka ====
 // getHTTPRule (pkg/envoy/server.go:261-320) + SortHeaderMatchers
 // (pkg/envoy/sort.go:205-250) + Envoy HeaderData construction.
-int build_http_rule(const l7m_http_rule& r, std::vector<HeaderData>* out, std::string* err) {
+int build_http_rule(const l7m_http_rule& r, std::vector<HeaderData>* out, std::string* err, int engine) {
   std::vector<Matcher> ms;
   if (!S(r.path).empty()) ms.push_back({":path", S(r.path), true});
   if (!S(r.method).empty()) ms.push_back({":method", S(r.method), true});
@@ -204,6 +222,17 @@ int build_http_rule(const l7m_http_rule& r, std::vector<HeaderData>* out, std::s
         *err = std::string("regex: ") + e.what();
         return L7M_EINVAL_REGEX;
       }
+      if (engine == 1) {
+        try {
+          hd.nfa = std::make_shared<const nfa::Prog>(nfa::compile(m.value));
+        } catch (const nfa::Unsupported& e) {
+          *err = std::string("nfa oracle: ") + e.what();
+          return L7M_EUNSUPPORTED;
+        } catch (const nfa::SyntaxError& e) {  // std::regex accepted it: the two parsers disagree
+          *err = std::string("nfa oracle parser disagrees with std::regex: ") + e.what();
+          return L7M_EUNSUPPORTED;
+        }
+      }
     } else hd.kind = 1;
     out->push_back(std::move(hd));
   }
@@ -220,7 +249,7 @@ bool match_headers(const std::vector<HeaderData>& hds, const HttpReq& q, bool se
         break;
       }
     if (!v) return false;
-    if (hd.kind == 0 && !(search ? std::regex_search(*v, hd.re) : std::regex_match(*v, hd.re))) return false;
+    if (hd.kind == 0 && !regex_ok(hd, *v, search)) return false;
     if (hd.kind == 1 && *v != hd.value) return false;
   }
   return true;
@@ -873,7 +902,7 @@ int32_t eval_kafka_one(const KafkaOracle& o, const KReq& q, uint64_t mask = ~0ul
 
 template <class F>
 void parallel_for(size_t n, int threads, F&& f) {
-  if (threads <= 1 || n < 1024) {
+  if (threads <= 1 || n < 2 * static_cast<size_t>(threads)) {
     for (size_t i = 0; i < n; ++i) f(i);
     return;
   }
@@ -890,14 +919,14 @@ void parallel_for(size_t n, int threads, F&& f) {
 
 extern "C" {
 
-int orc_http_new_dialect(const l7m_http_rule* rules, size_t n, uint32_t dialect, void** out, char* err,
-                         size_t errlen) {
+int orc_http_new_engine(const l7m_http_rule* rules, size_t n, uint32_t dialect, int engine, void** out, char* err,
+                        size_t errlen) {
   auto* o = new HttpOracle();
   o->search = dialect == L7M_DIALECT_RE2_SEARCH;
   for (size_t i = 0; i < n; ++i) {
     std::vector<HeaderData> hds;
     std::string e;
-    int rc = build_http_rule(rules[i], &hds, &e);
+    int rc = build_http_rule(rules[i], &hds, &e, engine);
     if (rc) {
       set_err(err, errlen, e);
       delete o;
@@ -912,11 +941,16 @@ int orc_http_new_dialect(const l7m_http_rule* rules, size_t n, uint32_t dialect,
   return L7M_OK;
 }
 
+int orc_http_new_dialect(const l7m_http_rule* rules, size_t n, uint32_t dialect, void** out, char* err,
+                         size_t errlen) {
+  return orc_http_new_engine(rules, n, dialect, 0, out, err, errlen);
+}
+
 // NetworkPolicyMap restated (envoy/cilium_network_policy.h:40-237,
 // npds.proto:32-118).  Verdict index = the flattened position of the deciding
 // HTTP rule in the order include/l7match.h (l7m_rule_origin) documents.
-int orc_http_policies_new(const l7m_network_policy* pols, size_t n, uint32_t dialect, void** out, char* err,
-                          size_t errlen) {
+int orc_http_policies_new_engine(const l7m_network_policy* pols, size_t n, uint32_t dialect, int engine, void** out,
+                                 char* err, size_t errlen) {
   auto* o = new PolicyOracle();
   o->search = dialect == L7M_DIALECT_RE2_SEARCH;
   int32_t index = 0;
@@ -951,7 +985,7 @@ int orc_http_policies_new(const l7m_network_policy* pols, size_t n, uint32_t dia
             for (size_t j = 0; j < R.n_http_rules; ++j) {
               std::vector<HeaderData> hds;
               std::string e;
-              int rc = build_http_rule(R.http_rules[j], &hds, &e);
+              int rc = build_http_rule(R.http_rules[j], &hds, &e, engine);
               if (rc) {
                 set_err(err, errlen, e);
                 delete o;
@@ -977,6 +1011,11 @@ int orc_http_policies_new(const l7m_network_policy* pols, size_t n, uint32_t dia
   }
   *out = o;
   return L7M_OK;
+}
+
+int orc_http_policies_new(const l7m_network_policy* pols, size_t n, uint32_t dialect, void** out, char* err,
+                          size_t errlen) {
+  return orc_http_policies_new_engine(pols, n, dialect, 0, out, err, errlen);
 }
 
 int orc_http_policies_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint64_t* offs, size_t n,
@@ -1016,6 +1055,19 @@ int orc_regex_search(const char* pattern, const char* input, size_t input_len) {
     return std::regex_search(std::string(input, input_len), re) ? 1 : 0;
   } catch (...) {
     return -1;
+  }
+}
+
+// The NFA simulator on one pattern: 1 / 0, -1 syntax error, -2 unsupported.
+int orc_nfa_match(const char* pattern, const char* input, size_t input_len, int search) {
+  try {
+    const nfa::Prog p = nfa::compile(pattern);
+    nfa::Runner run;
+    return run.run(p, reinterpret_cast<const uint8_t*>(input), input_len, search != 0) ? 1 : 0;
+  } catch (const nfa::SyntaxError&) {
+    return -1;
+  } catch (const nfa::Unsupported&) {
+    return -2;
   }
 }
 

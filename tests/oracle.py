@@ -21,6 +21,11 @@ def _load():
     lib.orc_http_new.argtypes = [ctypes.POINTER(L._HttpRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.orc_http_new_dialect.argtypes = [ctypes.POINTER(L._HttpRule), sz, ctypes.c_uint32, ctypes.POINTER(P),
                                          ctypes.c_char_p, sz]
+    lib.orc_http_new_engine.argtypes = [ctypes.POINTER(L._HttpRule), sz, ctypes.c_uint32, ctypes.c_int,
+                                        ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.orc_http_policies_new_engine.argtypes = [ctypes.POINTER(L._NetworkPolicy), sz, ctypes.c_uint32, ctypes.c_int,
+                                                 ctypes.POINTER(P), ctypes.c_char_p, sz]
+    lib.orc_nfa_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_int]
     lib.orc_http_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_http_free.argtypes = [P]
     lib.orc_http_policies_new.argtypes = [ctypes.POINTER(L._NetworkPolicy), sz, ctypes.c_uint32,
@@ -47,20 +52,27 @@ class OracleError(RuntimeError):
         self.code = code
 
 
+ENGINES = {"std": 0, "nfa": 1}
+
+
 class HttpOracle:
-    def __init__(self, rules, dialect=L.DIALECT_ENVOY_ECMA_FULL):
+    """engine="std": std::regex_match (the reference engine); engine="nfa":
+    the Thompson-NFA / Pike-VM simulator (oracle/nfa.h), the long-input oracle
+    for config 5 where the backtracker cannot finish or would overflow."""
+
+    def __init__(self, rules, dialect=L.DIALECT_ENVOY_ECMA_FULL, engine="std"):
         keep = []
         arr = (L._HttpRule * max(1, len(rules)))(*[L._http_rule_struct(r, keep) for r in rules])
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(512)
-        rc = _lib.orc_http_new_dialect(arr, len(rules), dialect, ctypes.byref(h), err, 512)
+        rc = _lib.orc_http_new_engine(arr, len(rules), dialect, ENGINES[engine], ctypes.byref(h), err, 512)
         if rc != 0:
             raise OracleError(rc, err.value.decode(errors="replace"))
         self._h = h
 
-    def __del__(self):
+    def __del__(self, _free=_lib.orc_http_free):  # bound early: module globals are gone at exit
         if getattr(self, "_h", None) and self._h.value:
-            _lib.orc_http_free(self._h)
+            _free(self._h)
 
     def eval(self, arena, offsets, threads=1):
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
@@ -74,19 +86,20 @@ class HttpOracle:
 class PolicyOracle:
     """NetworkPolicyMap restated (oracle/l7oracle.cc PolicyOracle)."""
 
-    def __init__(self, policies, dialect=L.DIALECT_ENVOY_ECMA_FULL):
+    def __init__(self, policies, dialect=L.DIALECT_ENVOY_ECMA_FULL, engine="std"):
         keep = []
         arr = L._policies_struct(policies, keep)
         h = ctypes.c_void_p()
         err = ctypes.create_string_buffer(512)
-        rc = _lib.orc_http_policies_new(arr, len(policies), dialect, ctypes.byref(h), err, 512)
+        rc = _lib.orc_http_policies_new_engine(arr, len(policies), dialect, ENGINES[engine], ctypes.byref(h), err,
+                                               512)
         if rc != 0:
             raise OracleError(rc, err.value.decode(errors="replace"))
         self._h = h
 
-    def __del__(self):
+    def __del__(self, _free=_lib.orc_http_policies_free):
         if getattr(self, "_h", None) and self._h.value:
-            _lib.orc_http_policies_free(self._h)
+            _free(self._h)
 
     def eval(self, arena, offsets, threads=1):
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
@@ -109,9 +122,9 @@ class KafkaOracle:
             raise OracleError(rc, err.value.decode(errors="replace"))
         self._h = h
 
-    def __del__(self):
+    def __del__(self, _free=_lib.orc_kafka_free):
         if getattr(self, "_h", None) and self._h.value:
-            _lib.orc_kafka_free(self._h)
+            _free(self._h)
 
     @classmethod
     def from_map(cls, entries, identities=None):
@@ -155,3 +168,8 @@ def regex_match(pattern: str, value: bytes) -> int:
 def regex_search(pattern: str, value: bytes) -> int:
     """std::regex_search(value, std::regex(pattern, optimize)) -> 1/0, -1 if invalid."""
     return _lib.orc_regex_search(pattern.encode(), value, len(value))
+
+
+def nfa_match(pattern: str, value: bytes, search: bool = False) -> int:
+    """The oracle's NFA simulator (oracle/nfa.h): 1/0, -1 syntax error, -2 unsupported."""
+    return _lib.orc_nfa_match(pattern.encode(), value, len(value), 1 if search else 0)

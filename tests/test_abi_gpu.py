@@ -43,3 +43,76 @@ def test_batcher_call_site_c_harness(gpu, tmp_path):
     batches, requests, denied, forwarded = (int(x) for x in st)
     assert requests == len(offs) and batches < requests // 4
     assert denied == int((exp == L.VERDICT_DENY).sum()) and forwarded == int((exp >= 0).sum())
+
+
+def test_pipelined_host_eval_large_batches(gpu):
+    """Host batches of >= 128 MiB take the chunked two-stream pipeline of
+    l7m_eval (H2D of chunk k+1 overlapping chunk k's kernel): verdicts and
+    counters equal the device-resident evaluation, HTTP and Kafka, pinned or
+    pageable host memory; an oracle sample pins the verdicts."""
+    import torch
+    for cfg, n in ((2, 1_500_000), (3, 2_200_000)):
+        rules = W.rules(cfg)
+        rs = L.RuleSet.compile_http(rules) if cfg == 2 else L.RuleSet.compile_kafka(rules)
+        arena, offs = W.requests(cfg, 9_000_000, n)
+        assert arena.nbytes >= (128 << 20), arena.nbytes  # the pipelined path
+        h = np.zeros(rs.n_counters, dtype=np.uint64)
+        v = rs.eval(arena, offs, h)
+        pinned = torch.from_numpy(arena).pin_memory().numpy()
+        h2 = np.zeros(rs.n_counters, dtype=np.uint64)
+        assert np.array_equal(rs.eval(pinned, offs, h2), v) and np.array_equal(h, h2)
+        dev = torch.device("cuda:0")
+        da = torch.from_numpy(arena).to(dev)
+        do = torch.from_numpy(offs.view(np.int64)).to(dev)
+        dv = torch.empty(len(offs), dtype=torch.int32, device=dev)
+        dh = torch.zeros(rs.n_counters, dtype=torch.int64, device=dev)
+        rs.eval_device(da, arena.nbytes, do, len(offs), dv, dh, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(dv.cpu().numpy(), v)
+        assert np.array_equal(dh.cpu().numpy().astype(np.uint64), h) and int(h.sum()) == n
+        # oracle on records spread over every chunk
+        from oracle import KafkaOracle
+        keep = np.arange(0, n, 997)
+        recs = [arena[int(offs[i]):int(offs[i + 1]) if i + 1 < n else arena.nbytes - 64].tobytes() for i in keep]
+        a2, o2 = L.pack_records(recs)
+        orc = HttpOracle(rules) if cfg == 2 else KafkaOracle(rules)
+        assert np.array_equal(orc.eval(a2, o2, threads=16), v[keep])
+
+
+def test_batcher_destroy_with_calls_in_flight(gpu):
+    """l7m_batcher_destroy while 64 threads are blocked inside
+    l7m_batcher_eval (a 2 s flush deadline keeps them waiting): the pending
+    batch is still decided, every caller gets the oracle's verdict, destroy
+    returns only after they have left, and a later call is L7M_EINVAL."""
+    import threading
+    import time
+    rules = W.rules(2)
+    rs = L.RuleSet.compile_http(rules)
+    arena, offs = W.requests(2, 11_000_000, 64)
+    exp = HttpOracle(rules).eval(arena, offs, threads=8)
+    recs = [arena[int(offs[i]):int(offs[i + 1]) if i + 1 < len(offs) else arena.nbytes - 64].tobytes()
+            for i in range(len(offs))]
+    for in_flight in (1, 3):
+        b = L.Batcher(rs, max_batch=1 << 20, max_delay_us=2_000_000, in_flight=in_flight)
+        got = np.full(len(recs), -100, dtype=np.int64)
+        entered = [False] * len(recs)
+
+        def worker(i):
+            entered[i] = True
+            got[i] = b.eval(recs[i])
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(len(recs))]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        while not all(entered):
+            time.sleep(0.001)
+        time.sleep(0.2)
+        b.close()  # flushes the pending batch now, not at the 2 s deadline
+        for x in th:
+            x.join()
+        assert time.perf_counter() - t0 < 1.5
+        assert np.array_equal(got, exp)
+        with pytest.raises(L.L7Error) as e:
+            b.eval(recs[0])
+        assert e.value.code == L.L7M_EINVAL

@@ -14,7 +14,7 @@ stop_if_fatal() {  # $1 = rc, $2 = step
   esac
 }
 echo "== pytest -m gpu" | tee -a $OUT/steps.log
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" | tee -a $OUT/steps.log; stop_if_fatal $rc pytest
 echo "== bench" | tee -a $OUT/steps.log
 timeout -k 10 420 python -u bench.py $BENCH_ARGS > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
