@@ -3,9 +3,21 @@ headline workload: config 2, 1k HTTP path/method/host/header regex rules,
 64M synthetic requests per GPU, inputs resident in HBM.
 
 One step = one l7m_eval_device pass over the rank's whole batch (+ the RCCL
-all-reduce of the per-rule hit/deny counters when N > 1).  Requests are
-sharded across ranks (each rank generates its own contiguous shard of the
-same deterministic workload), so scaling is weak.
+all-reduce of the per-rule hit/deny counters when N > 1).  The job's batch is
+one deterministic workload cut into contiguous byte-balanced shards
+(dist.balanced_shard); each rank generates its own shard.
+--scaling weak (default; config 4: strong): the job holds N x the per-GPU
+request count; strong: the job holds the config's request count, whatever N.
+
+At N = 1 the line also carries:
+  cpu_baseline  the oracle (reference algorithm restated) on all host cores
+                and on one, bounded sample (config 5: the NFA engine);
+  e2e           the host drop-in path: l7m_eval on a pinned host arena
+                (chunked H2D on two streams overlapped with the kernel, D2H
+                of verdicts): PCIe-inclusive verdicts/s;
+  batcher       per-request blocking calls (l7m_batcher_eval, the canAccess /
+                decodeHeaders call shape) from 8 / 64 / 512 caller threads:
+                verdicts/s and latency percentiles (cilium_amd/batcher_bench).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--requests R]
 N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -47,24 +59,50 @@ def parse():
     ap.add_argument("--lds-budget", type=int, default=0, help="bytes of rule tables kept in LDS (0 = default)")
     ap.add_argument("--mixed-streams", type=int, choices=[1, 2], default=1,
                     help="config 4: HIP streams for the two kernels (1 = back to back on one stream)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="weak: N x per-GPU requests (default); strong: the config's batch split over N "
+                         "(default for config 4, 'request batch sharded across 2/4/8')")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend (nccl = RCCL; gloo: the N>1 code path on one GPU in tests)")
+    ap.add_argument("--dump", default=None, help="write this rank's shard bounds + verdicts to DUMP.rank<r>.npz")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the pinned-host end-to-end leg")
+    ap.add_argument("--no-batcher", action="store_true", help="skip the per-request batcher leg")
+    ap.add_argument("--batcher-seconds", type=float, default=3.0)
     return ap.parse_args()
+
+
+def host_cores():
+    """CPUs this process may run on, the machine's count, and the cgroup CPU
+    quota (cores) when one is set."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "nproc": os.cpu_count(), "cgroup_quota_cores": quota}
 
 
 def cpu_baseline(cfg, rules, seconds, threads):
     """Oracle (the reference algorithm restated: per-request linear rule scan,
-    std::regex_match per matcher) timed on the host on a bounded sample."""
+    std::regex_match per matcher; K4 coverage for Kafka) timed on the host on a
+    bounded sample, on `threads` threads (all the host cores this process may
+    use) and on one.  Config 5 uses the oracle's NFA engine (oracle/nfa.h):
+    std::regex backtracks for seconds per request on the /f{i}/ family's
+    long tails and overflows its stack on long subjects, so
+    the unfiltered sample is timed with the linear-time engine."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import HttpOracle, KafkaOracle  # test infrastructure: cpu_baseline leg only
     proto = W.CONFIGS[cfg]["proto"]
-    orc = HttpOracle(rules) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+    engine = "nfa" if cfg == 5 else "std"
+    orc = HttpOracle(rules, engine=engine) if proto == L.PROTO_HTTP else KafkaOracle(rules)
     n0 = 20_000 if cfg != 5 else 16 * threads
 
     def sample(start, n):
-        a, o = W.requests(cfg, start, n, n_rules=len(rules), threads=threads)
-        if cfg == 5:  # std::regex backtracking: see tests/test_adversarial_gpu.py
-            from test_adversarial_gpu import cheap_for_oracle, subset
-            a, o = subset(a, o, cheap_for_oracle(a, o))
-        return a, o
+        return W.requests(cfg, start, n, n_rules=len(rules), threads=min(threads, 64))
 
     # calibrate on a small sample, then size the timed sample to ~`seconds`
     a, o = sample(10_000_000, n0)
@@ -82,13 +120,50 @@ def cpu_baseline(cfg, rules, seconds, threads):
     t = time.perf_counter()
     orc.eval(a1, o1, threads=1)
     dt1 = time.perf_counter() - t
-    note = "" if cfg != 5 else (" with /f{i}/ tails <= 24 bytes (longer ones make std::regex backtrack for "
-                                "seconds per request)")
+    hc = host_cores()
+    what = ("oracle/l7oracle.cc with the NFA engine (oracle/nfa.h; linear rule scan, Pike-VM full match)"
+            if engine == "nfa" else "oracle/l7oracle.cc (std::regex_match linear rule scan)"
+            if proto == L.PROTO_HTTP else "oracle/l7oracle.cc (ReadRequest + MatchesRule)")
     return {"value": len(o) / dt, "unit": "verdicts/s", "cores": threads, "kind": "port",
-            "single_thread_value": len(o1) / dt1, "cpu_model": cpu_model(),
-            "sample": f"{len(o)} requests of config {cfg} (from requests [20M, 20M+{n})){note}, {dt:.1f} s, "
-                      f"oracle/l7oracle.cc (std::regex_match linear rule scan) on {threads} threads; "
-                      f"single_thread_value: the first {len(o1)} of them on 1 thread, {dt1:.1f} s"}
+            "single_thread_value": len(o1) / dt1, "cpu_model": cpu_model(), "host": hc,
+            "sample": f"{len(o)} requests of config {cfg} (requests [20M, 20M+{n})), {dt:.1f} s, {what} "
+                      f"on {threads} threads (all {hc['affinity']} CPUs of this process' affinity; nproc "
+                      f"{hc['nproc']}, cgroup quota {hc['cgroup_quota_cores']}); single_thread_value: the "
+                      f"first {len(o1)} of them on 1 thread, {dt1:.1f} s"}
+
+
+def e2e_leg(rs, arena_pinned, offs, n, passes=2):
+    """PCIe-inclusive rate of the host drop-in path: l7m_eval on a pinned host
+    arena (the library cuts it into ~64 MiB chunks and overlaps chunk k+1's
+    H2D copy with chunk k's kernel on two streams, then copies the verdicts
+    back).  Inputs start on the host, verdicts end on the host."""
+    verd = np.empty(n, dtype=np.int32)
+    rs.eval(arena_pinned, offs, None)  # warm: device buffers of this size
+    t = time.perf_counter()
+    for _ in range(passes):
+        rs.eval(arena_pinned, offs, None)
+    dt = (time.perf_counter() - t) / passes
+    del verd
+    return {"verdicts_per_s": n / dt, "ms_per_batch": dt * 1e3, "host_GBps": arena_pinned.nbytes / dt / 1e9,
+            "requests": n, "passes": passes,
+            "path": "l7m_eval(pinned host arena): 64 MiB chunks, H2D on 2 streams overlapped with the kernel, "
+                    "D2H verdicts"}
+
+
+def batcher_leg(cfg, seconds):
+    """Per-request blocking calls through l7m_batcher (cilium_amd/batcher_bench,
+    a plain C client): verdicts/s and latency at 8 / 64 / 512 caller threads,
+    deadline batching (max_delay 200 us) and eager batching."""
+    import subprocess
+    exe = os.path.join(ROOT, "cilium_amd", "batcher_bench")
+    out = []
+    for eager in (1, 0):
+        p = subprocess.run([exe, str(cfg), "1000000", str(seconds), str(eager), "8", "64", "512"],
+                           capture_output=True, text=True, timeout=120)
+        if p.returncode != 0:
+            return {"error": p.stderr[-500:]}
+        out += [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    return out
 
 
 def cpu_model():
@@ -128,25 +203,34 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)  # ranks beyond the visible GPUs share them (gloo tests)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     cfg = args.config
+    scaling = args.scaling or ("strong" if cfg == 4 else "weak")
     if cfg == 4:
-        return run_mixed(args, world, rank, dev)
+        return run_mixed(args, world, rank, dev, scaling)
     c = W.CONFIGS[cfg]
-    per_gpu = args.requests or c["n_requests"]
-    threads = args.threads or max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    threads = args.threads or max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
+    n_job = (args.requests or c["n_requests"]) * (world if scaling == "weak" else 1)
 
     rules = W.rules(cfg)
     rs = (L.RuleSet.compile_http(rules, lds_budget_bytes=args.lds_budget) if c["proto"] == L.PROTO_HTTP
           else L.RuleSet.compile_kafka(rules))
 
-    # ---- rank's shard, generated deterministically, resident in HBM --------
-    log(f"rank {rank}: compiled {len(rules)} rules; generating {per_gpu} requests")
+    # ---- rank's byte-balanced shard, generated deterministically, in HBM ----
+    lo, hi = D.balanced_shard(cfg, n_job, world, rank, threads=threads,
+                              device=dev if args.backend == "nccl" else None)
+    per_gpu = hi - lo
+    log(f"rank {rank}: compiled {len(rules)} rules; generating requests [{lo}, {hi}) of {n_job}")
     t0 = time.perf_counter()
-    arena, offs = W.requests(cfg, rank * per_gpu, per_gpu, threads=threads)
+    arena, offs = W.requests(cfg, lo, per_gpu, threads=threads)
     gen_s = time.perf_counter() - t0
     rec_bytes = arena.nbytes - 64  # W.requests: packed (4-byte padded) records + 64 B tail pad
     pinned = torch.from_numpy(arena).pin_memory()
@@ -158,7 +242,11 @@ def main():
     h2d_s = time.perf_counter() - t0
     d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
     arena_nbytes = arena.nbytes
-    del pinned, arena, offs
+    keep_host = world == 1 and not args.no_e2e and not args.diag
+    host_offs = offs if keep_host else None
+    if not keep_host:
+        del pinned
+    del arena, offs
     d_verd = torch.empty(per_gpu, dtype=torch.int32, device=dev)
     d_hits = torch.zeros(rs.n_counters, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
@@ -192,12 +280,15 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    if args.dump:
+        np.savez(f"{args.dump}.rank{rank}.npz", lo=lo, hi=hi, verdicts=d_verd.cpu().numpy(),
+                 hits=d_hits.cpu().numpy(), elapsed=elapsed)
 
-    total_requests = per_gpu * world * args.steps
+    total_requests = n_job * args.steps
     value = total_requests / elapsed
     kavg = float(np.mean(kernel_ms)) / 1e3
     # algorithmic bytes per launch: records + u64 offset + i32 verdict per request (+ counters)
@@ -205,7 +296,7 @@ def main():
     achieved = alg_bytes / kavg / 1e9
     # sanity: verdicts were produced for every request of every step
     hits_total = int(d_hits.sum().item())
-    expect_hits = per_gpu * world
+    expect_hits = n_job
 
     if rank == 0:
         res = {
@@ -217,14 +308,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic generator libl7gen.so, SURVEY.md §8(d))",
             "config": {"workload": c["name"], "baseline_config": cfg, "n_rules": len(rules),
-                       "requests_per_gpu": per_gpu, "seed": hex(c["seed"]),
+                       "requests_per_gpu": per_gpu, "requests_total": n_job, "seed": hex(c["seed"]),
                        "mean_record_bytes": rec_bytes / per_gpu,
-                       "parallelism": f"dp{world} (request-sharded, RCCL all-reduce of {rs.n_counters} counters)",
+                       "parallelism": f"dp{world} (byte-balanced request shards, "
+                                      f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-reduce of "
+                                      f"{rs.n_counters} counters)",
                        "dfa_groups": int(rs.info.n_dfas), "dfa_states": int(rs.info.total_dfa_states)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
@@ -234,30 +327,41 @@ def main():
             "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
         }
         log(f"timed {args.steps} steps: {elapsed:.3f} s; kernel {kavg * 1e3:.2f} ms")
+        if keep_host:
+            log("end-to-end (pinned host arena)")
+            res["e2e"] = e2e_leg(rs, pinned.numpy(), host_offs, per_gpu)
+            del pinned
+        if world == 1 and not args.no_batcher and not args.diag and cfg in (2, 3) and not args.requests:
+            log("batcher (per-request calls)")
+            res["batcher"] = batcher_leg(cfg, args.batcher_seconds)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline")
-            res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds, threads)
+            res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds,
+                                               args.threads or len(os.sched_getaffinity(0)))
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def run_mixed(args, world, rank, dev):
-    """Config 4: 5k HTTP + 5k Kafka rules, 128M requests per GPU split by
-    protocol tag (W.mixed_parts), WEAK scaling like config 2: rank r
-    evaluates requests [r * n, (r + 1) * n) of each protocol's stream.  Per
+def run_mixed(args, world, rank, dev, scaling):
+    """Config 4: 5k HTTP + 5k Kafka rules, 128M requests split by protocol tag
+    (W.mixed_parts).  Strong scaling by default ("request batch sharded across
+    2/4/8"): the job is the config's 128M requests and rank r evaluates its
+    byte-balanced shard of each protocol's stream (--scaling weak: 128M per
+    GPU).  Per
     step the two kernels run back to back on one HIP stream (default; each is
     a persistent kernel sized to the whole GPU whose waves own fixed shares of
     the batch, so running them concurrently on two streams only delays the
     workgroups that start late: --mixed-streams 2), then one RCCL all-reduce
     sums the concatenated (R_http+2) + (R_kafka+2) counters."""
     c = W.CONFIGS[4]
-    threads = args.threads or max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
+    threads = args.threads or max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
     per_gpu = args.requests or c["n_requests"]
+    n_job_part = (per_gpu // 2) * (world if scaling == "weak" else 1)
     parts = []
     for proto, gcfg, seed, n_rules in W.mixed_parts(4):
-        n_part = per_gpu // 2
-        lo, hi = rank * n_part, (rank + 1) * n_part
+        lo, hi = D.balanced_shard(gcfg, n_job_part, world, rank, threads=threads, seed=seed, n_rules=n_rules,
+                                  device=dev if args.backend == "nccl" else None)
         rules = W.rules(gcfg, seed=seed, n_rules=n_rules)
         rs = (L.RuleSet.compile_http(rules, lds_budget_bytes=args.lds_budget) if proto == L.PROTO_HTTP
               else L.RuleSet.compile_kafka(rules))
@@ -309,12 +413,13 @@ def run_mixed(args, world, rank, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = [max(s.elapsed_time(e) for e in ends) for s, ends in evs]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    cdev = dev if args.backend == "nccl" else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     n_rank = sum(p["n"] for p in parts)
-    n_job = torch.tensor([n_rank], dtype=torch.int64, device=dev)
+    n_job = torch.tensor([n_rank], dtype=torch.int64, device=cdev)
     if world > 1:
         dist.all_reduce(n_job)
     n_job = int(n_job.item())
@@ -329,11 +434,11 @@ def run_mixed(args, world, rank, dev):
         "metric": f"L7 verdicts/sec ({c['name']}) + achieved HBM GB/s vs peak",
         "value": n_job * args.steps / elapsed,
         "unit": "verdicts/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (deterministic generator libl7gen.so, SURVEY.md §8(d))",
         "config": {"workload": c["name"], "baseline_config": 4, "n_rules": sum(len(p["rules"]) for p in parts),
-                   "requests_per_gpu": per_gpu, "requests_total": n_job, "seed": hex(c["seed"]),
+                   "requests_per_gpu": n_rank, "requests_total": n_job, "seed": hex(c["seed"]),
                    "parts": [{"generator_config": p["gcfg"], "n_rules": len(p["rules"]), "requests_rank0": p["n"],
                               "mean_record_bytes": p["rec_bytes"] / max(1, p["n"])} for p in parts],
                    "parallelism": f"dp{world} (request-sharded per protocol, {args.mixed_streams} HIP stream(s), "
@@ -345,6 +450,7 @@ def run_mixed(args, world, rank, dev):
         "counters_ok": counters_ok,
     }
     if world == 1 and not args.no_cpu_baseline:
+        threads = args.threads or len(os.sched_getaffinity(0))
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from oracle import HttpOracle, KafkaOracle  # test infrastructure: cpu_baseline leg only
         n_tot, t_tot, samples = 0, 0.0, []

@@ -12,7 +12,8 @@
 // request has waited max_delay_us, while the next batch fills.
 //
 // Pipelining: `in_flight` flusher threads (default 2) each take the next
-// ready batch, so batch k+1's H2D copy runs while batch k's kernel and D2H
+// ready batch (with `eager`, as soon as a flusher is free: batches then grow
+// with the load instead of waiting for max_delay_us), so batch k+1's H2D copy runs while batch k's kernel and D2H
 // run (l7m_eval is reentrant: every call has its own stream and device
 // buffers).  Batches live in pinned host memory (recycled, never freed while
 // the batcher lives), so the copies are DMA transfers, not staged.
@@ -86,6 +87,7 @@ struct l7m_batcher {
   uint32_t max_batch = 65536;
   uint32_t max_delay_us = 200;
   uint32_t in_flight = 2;
+  bool eager = false;  // flush as soon as a flusher is free (no deadline wait)
   int device = 0;
   Batch* cur = nullptr;
   std::vector<Batch*> pool;     // recycled batches (pinned buffers kept)
@@ -117,7 +119,8 @@ struct l7m_batcher {
       // full, or the first request has waited long enough (or shutting down)
       Batch* const b = cur;
       const auto deadline = b->first + std::chrono::microseconds(max_delay_us);
-      while (!stop && cur == b && b->offs.n < max_batch && Clock::now() < deadline) cv_flush.wait_until(lk, deadline);
+      while (!eager && !stop && cur == b && b->offs.n < max_batch && Clock::now() < deadline)
+        cv_flush.wait_until(lk, deadline);
       if (cur != b) continue;  // another flusher took it
       cur = fresh();
       l7m_ruleset* r = rs;
@@ -184,6 +187,7 @@ int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batche
     if (o.max_delay_us) b->max_delay_us = o.max_delay_us;
     if (k >= offsetof(l7m_batcher_opts, in_flight) + sizeof o.in_flight && o.in_flight)
       b->in_flight = o.in_flight > 8 ? 8 : o.in_flight;
+    if (k >= offsetof(l7m_batcher_opts, eager) + sizeof o.eager) b->eager = o.eager != 0;
     b->device = o.device;
   }
   b->cur = b->fresh();

@@ -64,7 +64,9 @@ EXPORTED_SYMBOLS = (
     "l7m_batcher_create", "l7m_batcher_set_ruleset", "l7m_batcher_eval", "l7m_batcher_eval_http",
     "l7m_batcher_stats", "l7m_batcher_destroy", "l7m_http_deny_body", "l7m_kafka_deny_response",
     "l7m_proxy_stats_add", "l7m_compile_kafka_map", "l7m_eval_ids", "l7m_eval_device_ids",
-    "l7m_batcher_eval_from",
+    "l7m_batcher_eval_from", "l7m_proxy_stats_table_create", "l7m_proxy_stats_table_destroy",
+    "l7m_proxy_stats_update", "l7m_proxy_stats_get", "l7m_http_access_log", "l7m_kafka_access_log",
+    "l7m_kafka_api_key_name",
 )
 
 
@@ -142,7 +144,21 @@ class _NetworkPolicy(ctypes.Structure):
 
 class _BatcherOpts(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("max_batch", ctypes.c_uint32),
-                ("max_delay_us", ctypes.c_uint32), ("device", ctypes.c_int32), ("in_flight", ctypes.c_uint32)]
+                ("max_delay_us", ctypes.c_uint32), ("device", ctypes.c_int32), ("in_flight", ctypes.c_uint32),
+                ("eager", ctypes.c_uint32)]
+
+
+class _AccessLogOpts(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("http_protocol", ctypes.c_uint32),
+                ("timestamp_ns", ctypes.c_uint64), ("policy_name", ctypes.c_char_p),
+                ("local_identity", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("source_address", ctypes.c_char_p), ("destination_address", ctypes.c_char_p)]
+
+
+class _KafkaLogRecord(ctypes.Structure):
+    _fields_ = [("request", ctypes.c_uint64), ("verdict", ctypes.c_uint32), ("error_code", ctypes.c_int32),
+                ("api_key", ctypes.c_int16), ("api_version", ctypes.c_int16), ("correlation_id", ctypes.c_int32),
+                ("topic_off", ctypes.c_uint64), ("topic_len", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class _ProxyStats(ctypes.Structure):
@@ -211,6 +227,17 @@ def _load() -> ctypes.CDLL:
     lib.l7m_http_deny_body.restype = sz
     lib.l7m_kafka_deny_response.argtypes = [ctypes.c_char_p, sz, P, sz, ctypes.POINTER(sz)]
     lib.l7m_proxy_stats_add.argtypes = [P, sz, ctypes.POINTER(_ProxyStats)]
+    lib.l7m_proxy_stats_table_create.restype = P
+    lib.l7m_proxy_stats_table_destroy.argtypes = [P]
+    lib.l7m_proxy_stats_update.argtypes = [P, ctypes.c_uint32, P, sz, P, P, sz, ctypes.c_uint16, ctypes.c_int]
+    lib.l7m_proxy_stats_get.argtypes = [P, P, sz]
+    lib.l7m_proxy_stats_get.restype = sz
+    lib.l7m_http_access_log.argtypes = [P, sz, P, sz, P, ctypes.POINTER(_AccessLogOpts), P, sz, P]
+    lib.l7m_http_access_log.restype = ctypes.c_int64
+    lib.l7m_kafka_access_log.argtypes = [P, sz, P, sz, P, P, sz]
+    lib.l7m_kafka_access_log.restype = ctypes.c_int64
+    lib.l7m_kafka_api_key_name.argtypes = [ctypes.c_int16, ctypes.c_char_p, sz]
+    lib.l7m_kafka_api_key_name.restype = sz
     lib.l7m_ruleset_rule_origin.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(_RuleOrigin)]
     lib.l7m_release.argtypes = [P]
     lib.l7m_release.restype = None
@@ -623,9 +650,10 @@ class Batcher:
     canAccess / decodeHeaders call shape, see include/l7match.h)."""
 
     def __init__(self, ruleset: "RuleSet", max_batch: int = 0, max_delay_us: int = 0, device: int = 0,
-                 in_flight: int = 0):
+                 in_flight: int = 0, eager: bool = False):
         self.ruleset = ruleset
-        opts = _BatcherOpts(ctypes.sizeof(_BatcherOpts), max_batch, max_delay_us, device, in_flight)
+        opts = _BatcherOpts(ctypes.sizeof(_BatcherOpts), max_batch, max_delay_us, device, in_flight,
+                            1 if eager else 0)
         h = ctypes.c_void_p()
         rc = _lib.l7m_batcher_create(ruleset.handle, ctypes.byref(opts), ctypes.byref(h))
         if rc != L7M_OK:
@@ -684,6 +712,92 @@ def proxy_stats(verdicts: np.ndarray) -> dict:
     st = _ProxyStats()
     _lib.l7m_proxy_stats_add(v.ctypes.data, v.shape[0], ctypes.byref(st))
     return {"received": st.received, "forwarded": st.forwarded, "denied": st.denied, "error": st.error}
+
+
+class _ProxyStatsEntry(ctypes.Structure):
+    _fields_ = [("proto", ctypes.c_uint32), ("port", ctypes.c_uint16), ("ingress", ctypes.c_uint8),
+                ("request", ctypes.c_uint8), ("stats", _ProxyStats)]
+
+
+class ProxyStatsTable:
+    """Endpoint.proxyStatistics keyed by (protocol, port, ingress, request)
+    (l7m_proxy_stats_table; pkg/endpoint/endpoint.go:2060-2122)."""
+
+    def __init__(self):
+        self._h = _lib.l7m_proxy_stats_table_create()
+
+    def __del__(self, _free=_lib.l7m_proxy_stats_table_destroy):
+        if getattr(self, "_h", None):
+            _free(self._h)
+
+    def update(self, proto: int, arena: np.ndarray, offsets: np.ndarray, verdicts: np.ndarray,
+               port: int = 0, ingress: bool = True) -> None:
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        v = np.ascontiguousarray(verdicts, dtype=np.int32)
+        rc = _lib.l7m_proxy_stats_update(self._h, proto, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
+                                         v.ctypes.data, v.shape[0], port, 1 if ingress else 0)
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_proxy_stats_update failed")
+
+    def entries(self) -> dict:
+        n = _lib.l7m_proxy_stats_get(self._h, None, 0)
+        arr = (_ProxyStatsEntry * max(1, n))()
+        _lib.l7m_proxy_stats_get(self._h, arr, n)
+        name = {PROTO_HTTP: "http", PROTO_KAFKA: "kafka"}
+        return {(name[e.proto], e.port, bool(e.ingress), bool(e.request)):
+                {"received": e.stats.received, "forwarded": e.stats.forwarded, "denied": e.stats.denied,
+                 "error": e.stats.error} for e in arr[:n]}
+
+
+def http_access_log(arena: np.ndarray, offsets: np.ndarray, verdicts: np.ndarray, policy_name: str = "",
+                    timestamp_ns: int = 0, http_protocol: int = 1, local_identity: int = 0,
+                    source_address: str = None, destination_address: str = None) -> List[bytes]:
+    """Serialized HttpLogEntry per request (l7m_http_access_log)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    v = np.ascontiguousarray(verdicts, dtype=np.int32)
+    n = v.shape[0]
+    o = _AccessLogOpts(ctypes.sizeof(_AccessLogOpts), http_protocol, timestamp_ns, _b(policy_name), local_identity,
+                       0, _b(source_address), _b(destination_address))
+    eo = np.zeros(n + 1, dtype=np.uint64)
+    need = _lib.l7m_http_access_log(arena.ctypes.data, arena.nbytes, offsets.ctypes.data, n, v.ctypes.data,
+                                    ctypes.byref(o), None, 0, eo.ctypes.data)
+    if need < 0:
+        raise L7Error(int(need), "l7m_http_access_log failed")
+    buf = ctypes.create_string_buffer(max(1, need))
+    got = _lib.l7m_http_access_log(arena.ctypes.data, arena.nbytes, offsets.ctypes.data, n, v.ctypes.data,
+                                   ctypes.byref(o), buf, need, eo.ctypes.data)
+    if got != need:
+        raise L7Error(L7M_EINVAL, "l7m_http_access_log size changed")
+    raw = buf.raw
+    return [raw[int(eo[i]):int(eo[i + 1])] for i in range(n)]
+
+
+def kafka_access_log(arena: np.ndarray, offsets: np.ndarray, verdicts: np.ndarray) -> List[dict]:
+    """The Kafka proxy's per-topic log records (l7m_kafka_access_log)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    v = np.ascontiguousarray(verdicts, dtype=np.int32)
+    n = _lib.l7m_kafka_access_log(arena.ctypes.data, arena.nbytes, offsets.ctypes.data, v.shape[0], v.ctypes.data,
+                                  None, 0)
+    if n < 0:
+        raise L7Error(int(n), "l7m_kafka_access_log failed")
+    arr = (_KafkaLogRecord * max(1, n))()
+    _lib.l7m_kafka_access_log(arena.ctypes.data, arena.nbytes, offsets.ctypes.data, v.shape[0], v.ctypes.data,
+                              arr, n)
+    names = ["Forwarded", "Denied", "Error"]
+    buf = arena.tobytes()
+    return [{"request": r.request, "verdict": names[r.verdict], "error_code": r.error_code,
+             "api_key": kafka_api_key_name(r.api_key), "api_version": r.api_version,
+             "correlation_id": r.correlation_id,
+             "topic": buf[r.topic_off:r.topic_off + r.topic_len].decode(errors="replace")} for r in arr[:n]]
+
+
+def kafka_api_key_name(key: int) -> str:
+    b = ctypes.create_string_buffer(64)
+    _lib.l7m_kafka_api_key_name(key, b, 64)
+    return b.value.decode()
 
 
 def matches_rule(records: Sequence[bytes], rules: Sequence[PortRuleKafka]) -> np.ndarray:

@@ -362,6 +362,9 @@ typedef struct {
   uint32_t max_delay_us; /* longest wait of a batch's first request (0 = 200) */
   int32_t device;        /* HIP device the batches run on                   */
   uint32_t in_flight;    /* batches evaluated concurrently (0 = 2, max 8)   */
+  uint32_t eager;        /* 1: a free flusher takes the pending requests at
+                            once (batch size follows the load; max_delay_us
+                            unused); 0: wait for max_batch / max_delay_us  */
 } l7m_batcher_opts;
 int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batcher** out);
 int l7m_batcher_set_ruleset(l7m_batcher* b, l7m_ruleset* rs);
@@ -398,6 +401,85 @@ typedef struct {
 size_t l7m_http_deny_body(const char* configured, char* out, size_t cap);
 int l7m_kafka_deny_response(const uint8_t* req, size_t len, uint8_t* out, size_t cap, size_t* out_len);
 int l7m_proxy_stats_add(const int32_t* verdicts, size_t n, l7m_proxy_stats* stats);
+
+/* Per-endpoint proxy statistics keyed as the endpoint keeps them
+ * (Endpoint.UpdateProxyStatistics(l7Protocol, port, ingress, request,
+ * verdict), pkg/endpoint/endpoint.go:2060-2122): one entry per (protocol,
+ * port, direction, request/response).  l7m_proxy_stats_update counts each
+ * request of a decided batch once, as the reference's call sites do:
+ *   HTTP  - port and direction from each record (the access-log entry's
+ *           DestinationEndpoint.Port / is_ingress, pkg/envoy/
+ *           accesslog_server.go:165-169); `port`, `ingress` unused;
+ *   Kafka - the redirect's port and direction (`port`, `ingress`); port 0
+ *           is not counted, nor a request ReadRequest rejected (the proxy
+ *           closes the connection) (pkg/proxy/kafka.go:213-229, 349-354).
+ * Verdicts: allowed -> forwarded, L7M_VERDICT_DENY -> denied, others ->
+ * error.  Thread-safe.  l7m_proxy_stats_get copies up to cap entries in key
+ * order and returns the number of entries. */
+typedef struct l7m_proxy_stats_table l7m_proxy_stats_table;
+typedef struct {
+  uint32_t proto;    /* L7M_PROTO_HTTP ("http") / L7M_PROTO_KAFKA ("kafka") */
+  uint16_t port;
+  uint8_t ingress;
+  uint8_t request;   /* 1: Statistics.Requests (verdicts are request-side)  */
+  l7m_proxy_stats stats;
+} l7m_proxy_stats_entry;
+l7m_proxy_stats_table* l7m_proxy_stats_table_create(void);
+void l7m_proxy_stats_table_destroy(l7m_proxy_stats_table* t);
+int l7m_proxy_stats_update(l7m_proxy_stats_table* t, uint32_t proto, const uint8_t* arena, size_t arena_bytes,
+                           const uint64_t* rec_offsets, const int32_t* verdicts, size_t n, uint16_t port,
+                           int ingress);
+size_t l7m_proxy_stats_get(l7m_proxy_stats_table* t, l7m_proxy_stats_entry* out, size_t cap);
+
+/* ---- access-log records of a decided batch ---------------------------------
+ * HTTP: the HttpLogEntry protobuf (envoy/cilium/accesslog.proto) Envoy's
+ * filter sends over the access-log socket for each request
+ * (AccessLog::Entry::InitFromRequest / UpdateFromResponse / AccessLog::Log,
+ * envoy/accesslog.cc:59-170; AccessFilter::decodeHeaders / encodeHeaders,
+ * envoy/cilium_l7policy.cc:166-191): EntryType Request for an allowed request,
+ * Denied with status 403 for a denied one; timestamp, http_protocol,
+ * policy_name, source_security_id (ingress: the record's remote identity,
+ * egress: opts->local_identity), addresses (when given), scheme (the
+ * x-forwarded-proto header), host / path / method, the other headers in
+ * request order, is_ingress.  Messages are written back to back into out;
+ * entry_offs[i] .. entry_offs[i+1] is request i's message (n + 1 entries;
+ * empty for records that do not parse).  Returns the total size (out == NULL:
+ * the size needed; L7M_ENOMEM when cap is too small). */
+typedef struct {
+  uint32_t struct_size;          /* sizeof(l7m_access_log_opts); 0 = defaults */
+  uint32_t http_protocol;        /* accesslog.proto Protocol: 0 HTTP10, 1 HTTP11 (default), 2 HTTP2 */
+  uint64_t timestamp_ns;         /* RequestInfo::startTime of the batch's requests */
+  const char* policy_name;       /* the filter's policy_name */
+  uint32_t local_identity;       /* egress: the local (source) endpoint's identity */
+  uint32_t reserved;
+  const char* source_address;    /* NULL: unset */
+  const char* destination_address;
+} l7m_access_log_opts;
+int64_t l7m_http_access_log(const uint8_t* arena, size_t arena_bytes, const uint64_t* rec_offsets, size_t n,
+                            const int32_t* verdicts, const l7m_access_log_opts* opts, uint8_t* out, size_t cap,
+                            uint64_t* entry_offs);
+/* Kafka: the proxy's log records (kafkaLogRecord.log, pkg/proxy/kafka.go
+ * :168-230; LogRecordKafka, pkg/proxy/accesslog/record.go:220-241): one
+ * record per topic of GetTopics() (none for requests without topics), verdict
+ * Forwarded / ErrorCode 0 for allowed requests, Denied / 29
+ * (ErrTopicAuthorizationFailed) for denied ones; requests ReadRequest rejects
+ * log nothing.  Topic names point into the arena.  Returns the number of
+ * records (out == NULL: the number needed; L7M_ENOMEM when cap is too small).
+ * l7m_kafka_api_key_name: apiKeyToString (pkg/proxy/kafka.go:161-166). */
+typedef struct {
+  uint64_t request;        /* index in the batch */
+  uint32_t verdict;        /* accesslog.FlowVerdict: 0 Forwarded, 1 Denied, 2 Error */
+  int32_t error_code;      /* Kafka.ErrorCode */
+  int16_t api_key;
+  int16_t api_version;
+  int32_t correlation_id;
+  uint64_t topic_off;      /* Kafka.Topic.Topic = arena[topic_off, topic_off + topic_len) */
+  uint32_t topic_len;
+  uint32_t pad;
+} l7m_kafka_log_record;
+int64_t l7m_kafka_access_log(const uint8_t* arena, size_t arena_bytes, const uint64_t* rec_offsets, size_t n,
+                             const int32_t* verdicts, l7m_kafka_log_record* out, size_t cap);
+size_t l7m_kafka_api_key_name(int16_t api_key, char* out, size_t cap);
 
 /* Pinned host memory helpers (cgo may not retain Go pointers across calls). */
 int l7m_alloc_pinned(size_t bytes, void** out);

@@ -36,7 +36,9 @@ def _worker(rank, world, port, cfg, n_rules, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rules = W.rules(cfg, n_rules=n_rules)
-    start, end = D.shard_bounds(N, world, rank)
+    # byte-balanced shard: block byte sums all-reduced over gloo (bench.py's path)
+    start, end = D.balanced_shard(cfg, N, world, rank, block=512, threads=1, n_rules=n_rules)
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), np.array([start, end]))
     arena, offs = W.requests(cfg, start, end - start, n_rules=n_rules, threads=1)
     orc = HttpOracle(rules) if cfg != 3 else KafkaOracle(rules)
     v = orc.eval(arena, offs)
@@ -62,6 +64,11 @@ def test_two_rank_sharded_counters_equal_single_process(tmp_path, cfg, n_rules):
         assert (np.load(tmp_path / f"ctr{r}.npy") == full).all()
     shards = np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(2)])
     assert (shards == v).all()  # shard invariance of the deterministic workload
+    b0, b1 = np.load(tmp_path / "b0.npy"), np.load(tmp_path / "b1.npy")
+    assert b0[0] == 0 and b0[1] == b1[0] and b1[1] == N
+    nbytes = arena.nbytes - 64
+    halves = [int(offs[b0[1]]), nbytes - int(offs[b0[1]])]
+    assert abs(halves[0] - halves[1]) < 0.01 * nbytes  # equal HBM bytes per rank
 
 
 def test_byte_balanced_bounds_cover_and_balance():
@@ -73,6 +80,23 @@ def test_byte_balanced_bounds_cover_and_balance():
         assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
         sizes = [(int(offs[e]) if e < len(offs) else nbytes) - int(offs[s]) for s, e in b]
         assert max(sizes) - min(sizes) <= 2 * 1024
+
+
+def test_block_byte_cuts_match_exact_byte_balance():
+    """dist.cuts_from_block_bytes (bench.py: block sums, interpolated) lands
+    within one block's imbalance of the exact per-record split."""
+    n = 50_000
+    arena, offs = W.requests(2, 0, n, n_rules=300)
+    nbytes = arena.nbytes - 64
+    for block in (256, 4096):
+        bb = W.block_bytes(2, 0, n, block, n_rules=300)
+        assert int(bb.sum()) == nbytes
+        for world in (2, 3, 8):
+            cuts = D.cuts_from_block_bytes(bb, block, n, world)
+            assert cuts[0][0] == 0 and cuts[-1][1] == n
+            assert all(cuts[i][1] == cuts[i + 1][0] for i in range(world - 1))
+            sizes = [(int(offs[e]) if e < n else nbytes) - int(offs[s]) for s, e in cuts]
+            assert max(sizes) - min(sizes) <= 0.02 * nbytes / world + 2048, (block, world, sizes)
 
 
 def test_counters_from_verdicts_semantics():

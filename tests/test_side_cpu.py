@@ -91,3 +91,101 @@ def test_kafka_deny_response_errors():
 def test_proxy_stats():
     v = np.array([0, 5, -1, -1, -2, -3, 7], dtype=np.int32)
     assert L.proxy_stats(v) == {"received": 7, "forwarded": 3, "denied": 2, "error": 2}
+
+
+# ---------------------------------------------------------------- access log --
+def _http_log_entry_class():
+    """cilium.HttpLogEntry built from envoy/cilium/accesslog.proto's field
+    numbers and types (transcribed schema; the library's bytes must parse and
+    re-serialize identically with the protobuf runtime)."""
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+    F = descriptor_pb2.FieldDescriptorProto
+    fp = descriptor_pb2.FileDescriptorProto(name="l7m_test_accesslog.proto", package="cilium", syntax="proto3")
+    kv = fp.message_type.add(name="KeyValue")
+    kv.field.add(name="key", number=1, type=F.TYPE_STRING, label=F.LABEL_OPTIONAL)
+    kv.field.add(name="value", number=2, type=F.TYPE_STRING, label=F.LABEL_OPTIONAL)
+    e = fp.message_type.add(name="HttpLogEntry")
+    for name, num, typ in [("timestamp", 1, F.TYPE_UINT64), ("http_protocol", 2, F.TYPE_UINT32),
+                           ("entry_type", 3, F.TYPE_UINT32), ("policy_name", 4, F.TYPE_STRING),
+                           ("cilium_rule_ref", 5, F.TYPE_STRING), ("source_security_id", 6, F.TYPE_UINT32),
+                           ("source_address", 7, F.TYPE_STRING), ("destination_address", 8, F.TYPE_STRING),
+                           ("scheme", 9, F.TYPE_STRING), ("host", 10, F.TYPE_STRING), ("path", 11, F.TYPE_STRING),
+                           ("method", 12, F.TYPE_STRING), ("status", 13, F.TYPE_UINT32)]:
+        e.field.add(name=name, number=num, type=typ, label=F.LABEL_OPTIONAL)
+    e.field.add(name="headers", number=14, type=F.TYPE_MESSAGE, type_name=".cilium.KeyValue",
+                label=F.LABEL_REPEATED)
+    e.field.add(name="is_ingress", number=15, type=F.TYPE_BOOL, label=F.LABEL_OPTIONAL)
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fp)
+    return message_factory.GetMessageClass(pool.FindMessageTypeByName("cilium.HttpLogEntry"))
+
+
+def test_http_access_log_entries():
+    """AccessLog::Entry::InitFromRequest / UpdateFromResponse / Log
+    (envoy/accesslog.cc:59-170) as AccessFilter drives them
+    (cilium_l7policy.cc:166-191): Request entries for allowed requests,
+    Denied + 403 for denied ones; x-forwarded-proto -> scheme; other headers
+    in order; identity by direction."""
+    Entry = _http_log_entry_class()
+    reqs = [L.HTTPRequest("GET", "/public/a", "svc.local", [("x-forwarded-proto", "https"), ("x-token", "12"),
+                                                            ("x-a", "1"), ("x-a", "2")], remote_id=7, ingress=True),
+            L.HTTPRequest("POST", "/private", None, [("user-agent", "curl")], remote_id=9, dport=8080, ingress=False),
+            L.HTTPRequest(None, None, None, [], remote_id=1)]
+    arena, offs = L.pack_http(reqs)
+    verdicts = np.array([3, L.VERDICT_DENY, L.VERDICT_ALLOW_NO_L7], dtype=np.int32)
+    msgs = L.http_access_log(arena, offs, verdicts, policy_name="ep-1", timestamp_ns=1_500_000_000_123,
+                             local_identity=4242, source_address="10.0.0.1:4000")
+    assert len(msgs) == 3
+    e = [Entry.FromString(m) for m in msgs]
+    for m, x in zip(msgs, e):
+        assert x.SerializeToString() == m  # canonical encoding (field order, proto3 defaults)
+    assert e[0].entry_type == 0 and e[0].status == 0 and e[0].is_ingress
+    assert (e[0].method, e[0].path, e[0].host, e[0].scheme) == ("GET", "/public/a", "svc.local", "https")
+    assert [(h.key, h.value) for h in e[0].headers] == [("x-token", "12"), ("x-a", "1"), ("x-a", "2")]
+    assert e[0].source_security_id == 7 and e[0].policy_name == "ep-1" and e[0].http_protocol == 1
+    assert e[0].timestamp == 1_500_000_000_123 and e[0].source_address == "10.0.0.1:4000"
+    assert e[0].cilium_rule_ref == ""  # this reference's filter does not set it
+    assert e[1].entry_type == 2 and e[1].status == 403 and not e[1].is_ingress
+    assert e[1].source_security_id == 4242  # egress: the local endpoint is the source
+    assert e[1].host == "" and [(h.key, h.value) for h in e[1].headers] == [("user-agent", "curl")]
+    assert e[2].method == "" and e[2].path == "" and e[2].entry_type == 0
+
+
+def test_kafka_access_log_records():
+    """kafkaLogRecord.log (pkg/proxy/kafka.go:168-230): one record per topic,
+    Forwarded/0 or Denied/29, apiKeyToString names; no record for requests
+    without topics or that ReadRequest rejects."""
+    recs = [K.produce(2, "cli", [("t1", [(0, b"")]), ("t2", [(1, b"")])]),
+            K.metadata(1, "cli", ["m1"]),
+            K.metadata(0, "cli", []),
+            K.consumer_metadata(0, "cli", "grp"),
+            K.generic(18, 0),
+            b"\x00\x00\x00\x02\x00\x00"]
+    arena, offs = L.pack_records(recs)
+    verdicts = np.array([0, L.VERDICT_DENY, 1, 2, L.VERDICT_DENY, L.VERDICT_PARSE_ERROR], dtype=np.int32)
+    out = L.kafka_access_log(arena, offs, verdicts)
+    assert [(r["request"], r["verdict"], r["error_code"], r["api_key"], r["api_version"], r["topic"]) for r in out] == [
+        (0, "Forwarded", 0, "produce", 2, "t1"), (0, "Forwarded", 0, "produce", 2, "t2"),
+        (1, "Denied", 29, "metadata", 1, "m1")]
+    assert all(r["correlation_id"] == 1 for r in out)
+    assert L.kafka_api_key_name(18) == "apiversions" and L.kafka_api_key_name(-5) == "-5"
+
+
+def test_proxy_stats_keyed_like_the_endpoint():
+    """UpdateProxyStatistics(l7Protocol, port, ingress, request, verdict)
+    (pkg/endpoint/endpoint.go:2099-2122): HTTP keyed by each record's dport and
+    direction, Kafka by the redirect's; Kafka port 0 and parse errors are not
+    counted."""
+    t = L.ProxyStatsTable()
+    reqs = [L.HTTPRequest("GET", "/", dport=80, ingress=True), L.HTTPRequest("GET", "/", dport=80, ingress=True),
+            L.HTTPRequest("GET", "/", dport=8080, ingress=False)]
+    arena, offs = L.pack_http(reqs)
+    t.update(L.PROTO_HTTP, arena, offs, np.array([0, L.VERDICT_DENY, L.VERDICT_ALLOW_NO_PORT_POLICY], np.int32))
+    karena, koffs = L.pack_records([K.metadata(0, "c", ["x"])] * 4)
+    kv = np.array([0, L.VERDICT_DENY, L.VERDICT_PARSE_ERROR, L.VERDICT_UNSUPPORTED], np.int32)
+    t.update(L.PROTO_KAFKA, karena, koffs, kv, port=9092, ingress=True)
+    t.update(L.PROTO_KAFKA, karena, koffs, kv, port=0, ingress=True)
+    e = t.entries()
+    assert e == {("http", 80, True, True): {"received": 2, "forwarded": 1, "denied": 1, "error": 0},
+                 ("http", 8080, False, True): {"received": 1, "forwarded": 1, "denied": 0, "error": 0},
+                 ("kafka", 9092, True, True): {"received": 3, "forwarded": 1, "denied": 1, "error": 1}}
