@@ -110,9 +110,11 @@ struct KafkaCodecDev {
 };
 KafkaCodecDev g_kcodec[64];
 
+// Decode slabs are 2 x maxParseBufSize + 64 KiB (~13 MB) per worker, allocated
+// at the first Kafka launch on a device: 16 workers ~ 211 MB.
 uint32_t codec_workers() {
   const char* e = std::getenv("L7M_KAFKA_CODEC_WORKERS");
-  const long v = e ? std::strtol(e, nullptr, 10) : 64;
+  const long v = e ? std::strtol(e, nullptr, 10) : 16;
   return v < 0 ? 0u : v > 4096 ? 4096u : static_cast<uint32_t>(v);
 }
 
@@ -147,16 +149,24 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
       g.cv.wait(lk);
     }
     slot->busy = true;
-    if (!slot->qhdr) {
+    if (!slot->qhdr || !slot->done) {  // first use, or a failed earlier initialisation: (re)try all of it
+      if (slot->qhdr) (void)hipFree(slot->qhdr);
+      if (slot->done) (void)hipEventDestroy(slot->done);
+      slot->qhdr = nullptr;
+      slot->done = nullptr;
       if (hipMalloc(reinterpret_cast<void**>(&slot->qhdr), 16) != hipSuccess ||
           hipEventCreateWithFlags(&slot->done, hipEventDisableTiming) != hipSuccess) {
+        if (slot->qhdr) (void)hipFree(slot->qhdr);
+        slot->qhdr = nullptr;
+        slot->done = nullptr;
         slot->busy = false;
+        g.cv.notify_one();
         return hipErrorOutOfMemory;
       }
-      if (g.workers &&
-          hipMalloc(reinterpret_cast<void**>(&slot->recs), kCodecQueueCap * sizeof(uint32_t)) == hipSuccess)
-        slot->cap = kCodecQueueCap;
     }
+    if (g.workers && !slot->recs &&
+        hipMalloc(reinterpret_cast<void**>(&slot->recs), kCodecQueueCap * sizeof(uint32_t)) == hipSuccess)
+      slot->cap = kCodecQueueCap;  // retried on later launches when it failed
     hipError_t e = hipStreamWaitEvent(stream, slot->done, 0);
     if (e == hipSuccess) e = hipMemsetAsync(slot->qhdr, 0, 16, stream);
     if (e != hipSuccess) {

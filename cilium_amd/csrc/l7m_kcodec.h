@@ -39,6 +39,10 @@ namespace l7m {
 enum CodecStatus : int { kCodecOk = 0, kCodecErr = 1, kCodecUnsupported = 2 };
 enum : uint32_t { kCodecGzip = 1, kCodecSnappy = 2 };
 constexpr uint32_t kCodecMaxDepth = 8;  // nested compressed sets followed per item
+// Decoded bytes the second pass produces for one request at most (two sets of
+// maxParseBufSize): past it values are reported unsupported, so one request
+// cannot hold the pass (and the launches chained behind it) for long.
+constexpr uint64_t kCodecRequestBudget = 2ull * static_cast<uint64_t>(kKafkaMaxParseBuf);
 
 __host__ __device__ inline uint32_t kc_crc_update(const uint32_t* tab, uint32_t c, const uint8_t* p, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) c = tab[(c ^ p[i]) & 0xffu] ^ (c >> 8);
@@ -442,10 +446,19 @@ struct KcFrame {
 // slab[top, ...) (top: the first free slab byte) and its set pushed (at most `max_sp` frames).  Returns at the
 // first value that fails (kCodecErr) or could not be decoded here
 // (kCodecUnsupported: nesting or slab limit).
+//
+// A value that cannot be decoded here (nesting, slab, or the request's
+// decode budget) does not stop the walk: the sets around it are still read
+// (their message boundaries do not depend on what a value decodes to), so a
+// later corrupt message still fails the request; the frames above st[0] are
+// dropped and the result is kCodecUnsupported unless something fails.
+// `budget`: decoded bytes this request may still produce (kc_check_produce).
 __host__ __device__ inline int kc_walk(KcFrame* st, uint32_t sp, uint32_t max_sp, uint32_t top, int16_t version,
                                        uint8_t* slab, uint32_t slab_bytes, const uint32_t* crc_tab,
-                                       KcInflateScratch& s) {
+                                       KcInflateScratch& s, uint64_t* budget) {
   const uint32_t max_out = static_cast<uint32_t>(kKafkaMaxParseBuf);
+  const uint32_t base_top = top;
+  bool unsup = false;
   int rc = kCodecOk;
   while (rc == kCodecOk && sp > 0) {
     KcFrame& f = st[sp - 1];
@@ -483,14 +496,15 @@ __host__ __device__ inline int kc_walk(KcFrame* st, uint32_t sp, uint32_t max_sp
           if (m.err) {
             rc = kCodecErr;
           } else if (comp != 0) {
-            if (sp >= max_sp) {
+            if (sp >= max_sp || *budget == 0) {
               rc = kCodecUnsupported;
             } else {
               uint32_t out = 0;
-              const uint32_t cap = slab_bytes - top;
+              const uint32_t cap = slab_bytes - top < *budget ? slab_bytes - top : static_cast<uint32_t>(*budget);
               rc = comp == kCodecGzip ? kc_gunzip(mb + vo, vl, slab + top, cap, max_out, &out, crc_tab, s)
                                       : kc_unsnappy(mb + vo, vl, slab + top, cap, max_out, &out);
               if (rc == kCodecOk) {
+                *budget -= out;
                 st[sp++] = KcFrame{slab + top, out, 0, top};
                 top += out;
               }
@@ -500,12 +514,19 @@ __host__ __device__ inline int kc_walk(KcFrame* st, uint32_t sp, uint32_t max_sp
       }
     }
     f.pos = r.pos;  // bytes of the set consumed so far (read by kc_check_produce)
+    if (rc == kCodecUnsupported) {  // skip what could not be decoded, keep reading st[0]
+      unsup = true;
+      rc = kCodecOk;
+      sp = 1;
+      top = base_top;
+      continue;
+    }
     if (pop) {
       top = st[sp - 1].slab_top;
       --sp;
     }
   }
-  return rc;
+  return rc == kCodecOk && unsup ? kCodecUnsupported : rc;
 }
 
 // Decode one compressed value into the slab and check the decoded set (and
@@ -520,7 +541,8 @@ __host__ __device__ inline int kc_check_value(const uint8_t* val, uint32_t vlen,
                                      : kc_unsnappy(val, vlen, slab, slab_bytes, max_out, &out);
   if (rc != kCodecOk) return rc;
   st[0] = KcFrame{slab, out, 0, 0};
-  return kc_walk(st, 1, kCodecMaxDepth, out, version, slab, slab_bytes, crc_tab, s);
+  uint64_t budget = kCodecRequestBudget;
+  return kc_walk(st, 1, kCodecMaxDepth, out, version, slab, slab_bytes, crc_tab, s, &budget);
 }
 
 // DecodeString (serialization.go:120-153), bytes skipped.
@@ -554,6 +576,7 @@ __host__ __device__ inline int kc_check_produce(const uint8_t* rec, uint32_t len
   kc_be(d, 6);                       // acks, timeout
   const int32_t nt = static_cast<int32_t>(kc_be(d, 4));
   int worst = kCodecOk;
+  uint64_t budget = kCodecRequestBudget;  // decoded bytes for the whole request (bounds the pass's time)
   for (int32_t t = 0; t < nt && !d.err; ++t) {
     kc_skip_str(d);  // topic
     const int32_t np = static_cast<int32_t>(kc_be(d, 4));
@@ -565,15 +588,11 @@ __host__ __device__ inline int kc_check_produce(const uint8_t* rec, uint32_t len
       const uint32_t avail = d.len - d.pos;
       KcFrame st[kCodecMaxDepth + 1];
       st[0] = KcFrame{d.p + d.pos, avail < static_cast<uint32_t>(mss) ? avail : static_cast<uint32_t>(mss), 0, 0};
-      const int rc = kc_walk(st, 1, kCodecMaxDepth + 1, 0, version, slab, slab_bytes, crc_tab, s);
+      const int rc = kc_walk(st, 1, kCodecMaxDepth + 1, 0, version, slab, slab_bytes, crc_tab, s, &budget);
       if (rc == kCodecErr) return rc;
-      if (rc == kCodecUnsupported) {
-        worst = rc;  // skip this set: a later one may still fail the request
-        break;
-      }
+      if (rc == kCodecUnsupported) worst = rc;  // the walk read the whole set: later sets may still fail
       d.pos += st[0].pos;  // the set's consumed bytes (a set stopped early leaves the rest)
     }
-    if (worst != kCodecOk) break;
   }
   return worst;
 }

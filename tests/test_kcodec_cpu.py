@@ -115,3 +115,53 @@ def test_second_pass_request_walk_matches_oracle_on_random_requests():
     mism = [(i, exp[i], got[i]) for i in range(len(recs)) if (got[i] == 1) != (exp[i] == -2) or got[i] == 2]
     assert not mism, mism[:10]
     assert 0 < sum(1 for e in exp if e == -2) < len(exp)
+
+
+def test_second_pass_continues_after_unsupported_set():
+    """a set the second pass cannot follow (9-deep nesting) does
+    not stop the request walk: a corrupt gzip set after it still fails the
+    request (-2, as ReadRequest would); with valid sets after it the result
+    stays unsupported (2); the 9-deep value inside a multi-message set does
+    not hide a corrupt message after it in the same set."""
+    lib = _kcodec()
+    deep = C.deep_nesting(9)  # a ProduceReq: take its message set back out
+    v = K.gzip_member(C.INNER)
+    for _ in range(8):
+        v = K.gzip_member(K.wrapper_set(v, K.GZIP, 1))
+    deep_set = K.wrapper_set(v, K.GZIP, 1)
+    ok = K.gzip_member(C.INNER)
+    corrupt_set = K.wrapper_set(ok[:-2], K.GZIP, 1)
+    good_set = K.wrapper_set(ok, K.GZIP, 1)
+    r_bad = K.produce(1, "c", [("t", [(0, deep_set), (1, corrupt_set)])])
+    r_good = K.produce(1, "c", [("t", [(0, deep_set)]), ("u", [(0, good_set)])])
+    r_same = K.produce(1, "c", [("t", [(0, deep_set + corrupt_set)])])
+    assert _oracle([r_bad, r_good, r_same]) == [-2, -1, -2]  # r_good decodes; topic u is not covered
+    assert lib.kc_host_check_produce(r_bad, len(r_bad), SLAB) == 1
+    assert lib.kc_host_check_produce(r_good, len(r_good), SLAB) == 2
+    assert lib.kc_host_check_produce(r_same, len(r_same), SLAB) == 1
+    assert deep  # the 9-deep request itself is covered by test_device_decoder_nesting_and_slab_limits
+
+
+def test_second_pass_decode_budget_bounds_a_gzip_bomb():
+    """a ProduceReq of many small gzip values that each inflate
+    to ~6 MB (a gzip bomb) is bounded by the per-request decode budget
+    (2 x maxParseBufSize): past it values are unsupported (reported, not
+    decoded); a corrupt value met within the budget still fails the request."""
+    import time
+    lib = _kcodec()
+    bomb = K.gzip_member(K.message_set(["a" * 6_000_000], version=1), level=9)
+    assert len(bomb) < 64 * 1024
+    sets = [K.wrapper_set(bomb, K.GZIP, 1) for _ in range(12)]
+    rec = K.produce(1, "c", [("t", [(i, s) for i, s in enumerate(sets)])])
+    t = time.perf_counter()
+    assert lib.kc_host_check_produce(rec, len(rec), SLAB) == 2
+    budget_s = time.perf_counter() - t
+    rec_bad = K.produce(1, "c", [("t", [(99, K.wrapper_set(bomb[:-3], K.GZIP, 1))] +
+                                  [(i, s) for i, s in enumerate(sets)])])
+    assert lib.kc_host_check_produce(rec_bad, len(rec_bad), SLAB) == 1
+    # 12 bombs = 72 MB decoded without the budget; with it ~13 MB
+    one = K.produce(1, "c", [("t", [(0, sets[0])])])
+    t = time.perf_counter()
+    assert lib.kc_host_check_produce(one, len(one), SLAB) == 0
+    one_s = time.perf_counter() - t
+    assert budget_s < 4 * one_s + 0.5, (budget_s, one_s)
