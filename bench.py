@@ -83,7 +83,8 @@ def host_cores():
                 quota = float(q) / float(per)
     except (OSError, ValueError):
         pass
-    return {"affinity": aff, "nproc": os.cpu_count(), "cgroup_quota_cores": quota}
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    return {"affinity": aff, "nproc": os.cpu_count(), "cgroup_quota_cores": quota, "usable": usable}
 
 
 def cpu_baseline(cfg, rules, seconds, threads):
@@ -127,9 +128,9 @@ def cpu_baseline(cfg, rules, seconds, threads):
     return {"value": len(o) / dt, "unit": "verdicts/s", "cores": threads, "kind": "port",
             "single_thread_value": len(o1) / dt1, "cpu_model": cpu_model(), "host": hc,
             "sample": f"{len(o)} requests of config {cfg} (requests [20M, 20M+{n})), {dt:.1f} s, {what} "
-                      f"on {threads} threads (all {hc['affinity']} CPUs of this process' affinity; nproc "
-                      f"{hc['nproc']}, cgroup quota {hc['cgroup_quota_cores']}); single_thread_value: the "
-                      f"first {len(o1)} of them on 1 thread, {dt1:.1f} s"}
+                      f"on {threads} threads = every core this process can use (affinity {hc['affinity']} CPUs, "
+                      f"nproc {hc['nproc']}, cgroup CPU quota {hc['cgroup_quota_cores']} cores); "
+                      f"single_thread_value: the first {len(o1)} of them on 1 thread, {dt1:.1f} s"}
 
 
 def e2e_leg(rs, arena_pinned, offs, n, passes=2):
@@ -337,7 +338,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds,
-                                               args.threads or len(os.sched_getaffinity(0)))
+                                               args.threads or host_cores()["usable"])
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -450,7 +451,7 @@ def run_mixed(args, world, rank, dev, scaling):
         "counters_ok": counters_ok,
     }
     if world == 1 and not args.no_cpu_baseline:
-        threads = args.threads or len(os.sched_getaffinity(0))
+        threads = args.threads or host_cores()["usable"]
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from oracle import HttpOracle, KafkaOracle  # test infrastructure: cpu_baseline leg only
         n_tot, t_tot, samples = 0, 0.0, []

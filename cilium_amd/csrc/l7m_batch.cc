@@ -21,6 +21,7 @@
 // pkg/proxy/redirect.go:68-74): batches flushed afterwards use the new rules.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstddef>
 #include <condition_variable>
@@ -61,12 +62,17 @@ struct PinnedVec {
   }
 };
 
+// A batch's completion has its own mutex / condition variable, so finishing
+// one batch wakes only its callers (no thundering herd across batches) and
+// they do not contend with callers appending to the next batch.
 struct Batch {
   PinnedVec<uint8_t> arena;
   PinnedVec<uint64_t> offs;
   PinnedVec<uint32_t> ids;  // source identities (Kafka rule sets)
   PinnedVec<int32_t> verd;
   Clock::time_point first;
+  std::mutex m;             // guards done, rc, waiters
+  std::condition_variable cv;
   bool done = false;
   int rc = L7M_OK;
   uint32_t waiters = 0;  // callers that have not read their verdict yet
@@ -81,8 +87,8 @@ struct Batch {
 }  // namespace
 
 struct l7m_batcher {
-  std::mutex mu;
-  std::condition_variable cv_flush, cv_done, cv_idle;
+  std::mutex mu;  // guards cur, pool, rs, stop, stats (lock order: mu, then a batch's m)
+  std::condition_variable cv_flush, cv_idle;
   l7m_ruleset* rs = nullptr;
   uint32_t max_batch = 65536;
   uint32_t max_delay_us = 200;
@@ -93,7 +99,7 @@ struct l7m_batcher {
   std::vector<Batch*> pool;     // recycled batches (pinned buffers kept)
   std::vector<Batch*> all;      // every batch ever made (freed at destroy)
   bool stop = false;
-  uint32_t callers = 0;         // threads inside eval()
+  std::atomic<uint32_t> callers{0};  // threads inside eval()
   uint64_t batches = 0, requests = 0;
   std::vector<std::thread> flushers;
 
@@ -137,11 +143,13 @@ struct l7m_batcher {
                           info.proto == L7M_PROTO_KAFKA ? b->ids.p : nullptr, b->verd.p, nullptr, 0);
       }
       l7m_release(r);
+      {
+        std::lock_guard<std::mutex> g(b->m);
+        b->rc = rc;
+        b->done = true;
+      }
+      b->cv.notify_all();
       lk.lock();
-      b->rc = rc;
-      b->done = true;
-      if (b->waiters == 0) pool.push_back(b);
-      cv_done.notify_all();
     }
   }
 
@@ -154,7 +162,7 @@ struct l7m_batcher {
     // + 64 bytes of zero tail for the kernels' aligned loads (l7m_eval pads its copy too)
     if (!b->arena.reserve(off + padded + 64) || !b->offs.reserve(idx + 1) || !b->ids.reserve(idx + 1))
       return L7M_ENOMEM;
-    ++callers;
+    callers.fetch_add(1);
     if (idx == 0) b->first = Clock::now();
     b->offs.p[idx] = off;
     b->ids.p[idx] = src_identity;
@@ -162,13 +170,30 @@ struct l7m_batcher {
     std::memset(b->arena.p + off + len, 0, padded - len);
     b->arena.n = off + padded;
     b->offs.n = idx + 1;
-    ++b->waiters;
+    {
+      std::lock_guard<std::mutex> g(b->m);  // b is not in flight yet: done is false
+      ++b->waiters;
+    }
     if (idx == 0 || b->offs.n >= max_batch) cv_flush.notify_one();
-    cv_done.wait(lk, [&] { return b->done; });
-    const int rc = b->rc;
-    if (rc == L7M_OK) *verdict = b->verd.p[idx];
-    if (--b->waiters == 0) pool.push_back(b);  // the last reader recycles it
-    if (--callers == 0) cv_idle.notify_all();
+    lk.unlock();
+    int rc;
+    bool last;
+    {
+      std::unique_lock<std::mutex> bl(b->m);
+      b->cv.wait(bl, [&] { return b->done; });
+      rc = b->rc;
+      if (rc == L7M_OK) *verdict = b->verd.p[idx];
+      last = --b->waiters == 0;
+    }
+    if (last) {  // the last reader recycles the batch
+      lk.lock();
+      pool.push_back(b);
+      lk.unlock();
+    }
+    if (callers.fetch_sub(1) == 1) {
+      std::lock_guard<std::mutex> g(mu);
+      cv_idle.notify_all();
+    }
     return rc;
   }
 };
@@ -253,7 +278,7 @@ void l7m_batcher_destroy(l7m_batcher* b) {
     if (t.joinable()) t.join();
   {
     std::unique_lock<std::mutex> lk(b->mu);
-    b->cv_idle.wait(lk, [&] { return b->callers == 0; });
+    b->cv_idle.wait(lk, [&] { return b->callers.load() == 0; });
   }
   l7m_release(b->rs);
   for (Batch* x : b->all) delete x;

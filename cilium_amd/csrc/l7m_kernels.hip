@@ -773,6 +773,7 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
     t.take = t.k ? t.k : 1u;
     return t;
   };
+#ifdef L7M_REGSTAGE
   u32x4 buf[kCopyIters];
   auto issue_bytes = [&](const Tile& t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
@@ -782,17 +783,41 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
       if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
     }
   };
+#else
+  // LDS-DMA staging (global_load_lds_dwordx4, non-temporal): the tile's bytes
+  // go HBM -> the wave's stage with no VGPR destination and no ds_write pass;
+  // lane l of piece `it` lands at stage + it * 1 KiB + 16 l (the coalesced
+  // copy's own layout).  Issued after the walks, the only readers of the
+  // stage; the next loop iteration waits for it before reading.
+  auto issue_bytes = [&](const Tile& t) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's stage reads are done
+#pragma unroll
+    for (uint32_t it = 0; it < kCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < t.bytes)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(stg + it * 1024u)),
+                                         16, 0, 2);
+    }
+  };
+#endif
   uint64_t o1, n1, o2, n2;
   load_offs(n * gw / nw, &o1, &n1);
   Tile t = plan(n * gw / nw, o1, n1);
   issue_bytes(t);
   load_offs(t.cur + t.take, &o2, &n2);
   while (t.cur < end) {
+#ifdef L7M_REGSTAGE
 #pragma unroll
     for (uint32_t it = 0; it < kCopyIters; ++it) {
       const uint32_t q = it * 64u + lane;
       if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
     }
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
+#endif
     wave_sync();
 
     const uint64_t o = t.o, onext = t.onext, base = t.base;
