@@ -557,8 +557,68 @@ re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const Fi
     return res[r].accept[t - rbase[r] + 1] ? kLatchedAccept : 0;
   };
 
-  // 5. placement: product rows below `region`, tails at or above; dense rows
-  // of each phase first
+  // 4b. skip rows (dfa_pack.h kSkipLoop / kSkipLit) among the tails: loop
+  // rows, and literal runs of >= 2 bytes starting at a residual state or at a
+  // chain node entered from >= 2 rows (the shared, hot ones: config 2's
+  // `\.ns\.local` authority suffix, `(users|orders|items)/`); placed last so
+  // that `base >= skip_lim` identifies them.
+  std::vector<uint8_t> skind(nrows, 0);  // 1 loop, 2 one non-accepting transition to another row
+  std::vector<uint32_t> snext(nrows, 0);
+  std::vector<uint32_t> indeg(nrows, 0);
+  for (uint32_t r = 1; r < nrows; ++r) {
+    row_bytes(r);
+    for (const auto& x : rb) ++indeg[x.row];
+    if (r <= nmulti) continue;
+    bool loop = true;
+    for (const auto& x : rb) loop &= x.row == r;
+    if (loop) skind[r] = 1;
+    else if (rb.size() == 1 && row_accept(r) == 0) {
+      skind[r] = 2;
+      snext[r] = rb[0].row;
+    }
+  }
+  std::vector<uint8_t> runlen(nrows, 0);  // literal run length from a kind-2 row (capped)
+  for (uint32_t r = 1 + nmulti; r < nrows; ++r) {
+    if (skind[r] != 2 || runlen[r]) continue;
+    std::vector<uint32_t> path;
+    uint32_t c = r;
+    while (c && skind[c] == 2 && !runlen[c] && path.size() < 64) {
+      runlen[c] = 0xff;  // on the current path (cycle guard)
+      path.push_back(c);
+      c = snext[c];
+    }
+    uint32_t tail_len = (c && skind[c] == 2 && runlen[c] != 0xff) ? runlen[c] : 0;
+    for (size_t i = path.size(); i-- > 0;) {
+      tail_len = tail_len + 1 > kSkipMaxLit ? kSkipMaxLit : tail_len + 1;
+      runlen[path[i]] = static_cast<uint8_t>(tail_len);
+    }
+  }
+  std::vector<uint8_t> has_skip(nrows, 0);
+  {
+    uint32_t nrows_skip = 0, pool = 0;
+    for (uint32_t r = 1 + nmulti; r < nrows && nrows_skip < kSkipMaxRows; ++r)
+      if (skind[r] == 1) {
+        has_skip[r] = 1;
+        ++nrows_skip;
+      }
+    // hot runs: rows of residual automata, chain nodes entered from >= 2 rows,
+    // and every later row of a hot run (a block boundary can land anywhere in it)
+    std::vector<uint8_t> hot(nrows, 0);
+    for (uint32_t r = 1 + nmulti; r < nrows; ++r) {
+      if (skind[r] != 2 || hot[r] || !(tail_kind[r - 1 - nmulti] == 1 || indeg[r] >= 2)) continue;
+      for (uint32_t c = r, i = 0; c && skind[c] == 2 && !hot[c] && i < 64; c = snext[c], ++i) hot[c] = 1;
+    }
+    for (uint32_t r = 1 + nmulti; r < nrows && nrows_skip < kSkipMaxRows; ++r) {
+      if (skind[r] != 2 || runlen[r] < 2) continue;
+      if (!hot[r] || pool + runlen[r] > kSkipMaxPool) continue;
+      has_skip[r] = 1;
+      ++nrows_skip;
+      pool += runlen[r];
+    }
+  }
+
+  // 5. placement: product rows below `region`, tails at or above (skip rows
+  // last); dense rows of each phase first
   std::vector<uint32_t> base(nrows, 0);
   std::vector<uint16_t> cnt(nrows, 0);
   uint64_t n_explicit = 0;
@@ -572,10 +632,11 @@ re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const Fi
   pk.reserve_base(0);  // dead
   uint32_t max_base = 0;
   std::vector<uint8_t> bytes;
-  auto place_phase = [&](uint32_t lo_row, uint32_t hi_row, uint32_t lo_base) -> bool {
+  auto place_phase = [&](uint32_t lo_row, uint32_t hi_row, uint32_t lo_base, int skip_sel) -> bool {
     pk.begin_phase(lo_base);
     std::vector<std::vector<uint32_t>> by(257);
-    for (uint32_t r = lo_row; r < hi_row; ++r) by[cnt[r]].push_back(r);
+    for (uint32_t r = lo_row; r < hi_row; ++r)
+      if (skip_sel < 0 || has_skip[r] == skip_sel) by[cnt[r]].push_back(r);
     for (int c = 256; c >= 0; --c)
       for (uint32_t r : by[c]) {
         row_bytes(r);
@@ -587,9 +648,13 @@ re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const Fi
     return true;
   };
   tr.mark("rows", nrows);
-  if (!place_phase(1, 1 + nmulti, 1)) return re::Status::TooBig;
+  if (!place_phase(1, 1 + nmulti, 1, -1)) return re::Status::TooBig;
   const uint32_t region = max_base + 1;
-  if (!place_phase(1 + nmulti, nrows, region)) return re::Status::TooBig;
+  if (!place_phase(1 + nmulti, nrows, region, 0)) return re::Status::TooBig;
+  const uint32_t skip_lim = max_base + 1;
+  bool any_skip = false;
+  for (uint32_t r = 1 + nmulti; r < nrows; ++r) any_skip |= has_skip[r] != 0;
+  if (any_skip && !place_phase(1 + nmulti, nrows, skip_lim, 1)) return re::Status::TooBig;
   tr.mark("placement", max_base);
 
   // 6. tables
@@ -610,6 +675,27 @@ re::Status build_field_dfa(const std::vector<const re::Ast*>& patterns, const Fi
     d.es[base[r]] = row_accept(r);
   }
   tr.mark("tables", d.n_slots);
+  if (any_skip) {
+    d.skip_lim = skip_lim;
+    d.skip.assign(max_base + 1 - skip_lim, 0u);
+    for (uint32_t r = 1 + nmulti; r < nrows; ++r) {
+      if (!has_skip[r]) continue;
+      uint32_t w = kSkipLoop;
+      if (skind[r] == 2) {
+        const uint32_t n = runlen[r], off = static_cast<uint32_t>(d.skip_lits.size());
+        uint32_t c = r, tslot = 0;
+        for (uint32_t i = 0; i < n; ++i) {  // the run's bytes; tslot = its last transition's slot
+          row_bytes(c);
+          d.skip_lits.push_back(rb[0].b);
+          tslot = base[c] + rb[0].b;
+          c = rb[0].row;
+        }
+        w = kSkipLit | n << 2 | off << 7 | tslot << 16;
+        if (tslot >= (1u << 16)) w = 0;  // beyond an LDS table's reach: no skip
+      }
+      d.skip[base[r] - skip_lim] = w;
+    }
+  }
   d.start_base = start_row == 0 ? 0u : base[row_of(start_row)];
   d.start_latch = start_latch;
   d.region = region;

@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "program.h"
 #include "regex_ecma.h"
 
 namespace l7m {
@@ -54,7 +55,23 @@ struct PackedDfa {
   uint32_t n_multi = 0;          // multi-pattern (product) states
   uint32_t n_residuals = 0;      // distinct residual automata
   std::vector<std::vector<uint32_t>> sets;  // end sets (set id -> sorted pattern ids), set 0 empty
+  // Skip descriptors of latched rows (the walk's fast paths, see skip_kind):
+  // every row with base >= skip_lim has one, skip[base - skip_lim]; 0 = none.
+  uint32_t skip_lim = 0;              // 0: no skip rows
+  std::vector<uint32_t> skip;         // per base in [skip_lim, max base]
+  std::vector<uint8_t> skip_lits;     // literal pool of kSkipLit rows
 };
+
+// Skip descriptor word (latched rows only, so slast is unaffected):
+//   kSkipLoop: every transition of the row returns to the row itself: the
+//     rest of the field stays in the row iff each byte b has T[base + b]
+//     labelled b (independent lookups), else the walk is dead.
+//   kSkipLit:  the row starts a run of n >= 2 non-accepting single-transition
+//     rows (a literal): the next n bytes must equal skip_lits[off, off + n)
+//     (else dead; a field ending inside the run does not match either), and
+//     the walk continues from the entry T[tslot] (the run's last transition).
+//   word = kind | n << 2 | off << 7 | tslot << 16   (n <= 31, off < 512, tslot < 64 Ki)
+// (kSkipLoop / kSkipLit and the limits are in program.h, shared with the kernels)
 
 struct FieldDfaLimits {
   size_t max_multi_states = 1u << 21;  // product states before the caller splits the pattern set

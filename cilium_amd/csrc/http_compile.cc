@@ -427,6 +427,8 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     dd[k].lds_table = dd[k].lds_es = dd[k].lds_latch = dd[k].lds_ct = dd[k].lds_mask = kNone;
     dd[k].lds_ctmask = kNone;
     dd[k].lit_tab = kNone;
+    dd[k].lds_skip = kNone;
+    dd[k].skip_lim = 0;
     total_states += d.nstates;
     for (size_t s = 0; s < d.sets.size(); ++s) {
       sets.push_back(push_list(d.sets[s]));
@@ -560,6 +562,15 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       // the slot table (read once per byte) alone; end codes / latches (read
       // once per walk) stay in the program
       dd[k].lds_table = img_take(d.n_slots);
+    }
+    // skip descriptors (dfa_pack.h): the literal pool, then one word per
+    // skip-row base; only with the table in LDS and when they fit too
+    const uint64_t pool_words = ((d.skip_lits.size() + 3) / 4 + 3) & ~uint64_t(3);  // img_take granules
+    if (dd[k].lds_table != kNone && d.skip_lim && d.skip_lim < (1u << 16) && pool_words < (1u << 15) &&
+        img + pool_words + d.skip.size() + 8 <= budget) {
+      img_take(pool_words);
+      dd[k].lds_skip = img_take(d.skip.size());
+      dd[k].skip_lim = d.skip_lim | static_cast<uint32_t>(pool_words) << 16;
     }
   }
   // Candidate tables are read once per request (after the walks), so they
@@ -718,6 +729,11 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
                          : (t0 << kLdsRowShift);
       }
       if (in_entry && d.start_base) dd[k].start_es8 = es8(d.start_base);
+      if (dd[k].lds_skip != kNone) {
+        std::memcpy(I + dd[k].lds_skip, d.skip.data(), d.skip.size() * 4);
+        std::memcpy(reinterpret_cast<uint8_t*>(I + dd[k].lds_skip - (dd[k].skip_lim >> 16)), d.skip_lits.data(),
+                    d.skip_lits.size());
+      }
       for (uint32_t s = 0; dd[k].lds_es != kNone && !in_entry && s < d.n_slots; ++s)
         I16[dd[k].lds_es + s] = d.es[s] == kLatchedAccept ? static_cast<uint16_t>(kEs16Latched)
                                                            : static_cast<uint16_t>(d.es[s]);

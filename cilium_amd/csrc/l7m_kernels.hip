@@ -185,11 +185,69 @@ __device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, c
 // slot of the last transition taken from a multi-pattern row (below lim).
 struct LdsChain {
   uint32_t sel, dead, lim, slast;
+  uint32_t slim;  // rows >= slim carry skip descriptors (dfa_pack.h), ~0u: none
+  uint32_t sk;    // LDS word of the descriptor of row slim
+  uint32_t lw;    // LDS word of the literal pool
   __device__ __forceinline__ void init(const DfaDesc& dd) {
     dead = dd.lds_table << kLdsRowShift;
     lim = dd.lds_table + dd.region;
     sel = ((dd.lds_table + dd.start_base) << kLdsRowShift) | (dd.start_es8 << 8);
     slast = kNone;
+#ifndef L7M_NO_SKIP
+    slim = dd.lds_skip != kNone ? dd.lds_table + (dd.skip_lim & 0xffffu) : ~0u;
+    sk = dd.lds_skip;
+    lw = dd.lds_skip - (dd.skip_lim >> 16);
+#else
+    slim = ~0u;
+    sk = lw = 0;
+#endif
+  }
+  // Skip rows (latched, so slast is unaffected): a loop row decides the rest
+  // of the field with independent lookups; a literal run is compared with
+  // its bytes and the walk jumps past it.  Called for lanes whose row is
+  // >= slim at a block boundary; returns the new k (len when decided).
+  template <class Src>
+  __device__ __forceinline__ uint32_t skip(const uint32_t* __restrict__ img, const Src& src, uint32_t pos, uint32_t len,
+                                        uint32_t k) {
+    const uint32_t t0 = dead >> kLdsRowShift;
+    for (uint32_t guard = 0; guard < 64; ++guard) {
+      const uint32_t row = sel >> kLdsRowShift;
+      if (row < slim || sel == dead || k >= len) return k;
+      const uint32_t w = img[sk + (row - slim)];
+      if (w & kSkipLoop) {  // every byte must be one of the row's own labels
+        uint32_t bad = 0;
+        for (; k + 4 <= len; k += 4) {
+          const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
+          const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
+          bad |= (img[row + b0] ^ b0) & 0xffu;
+          bad |= (img[row + b1] ^ b1) & 0xffu;
+          bad |= (img[row + b2] ^ b2) & 0xffu;
+          bad |= (img[row + b3] ^ b3) & 0xffu;
+        }
+        for (; k < len; ++k) {
+          const uint32_t b = src.byte(pos + k);
+          bad |= (img[row + b] ^ b) & 0xffu;
+        }
+        if (bad) sel = dead;
+        return len;
+      }
+      if (!(w & kSkipLit)) return k;
+      const uint32_t n = (w >> 2) & 31u, off = (w >> 7) & 511u;
+      if (len - k < n) {  // ends inside the literal run (non-accepting rows)
+        sel = dead;
+        return len;
+      }
+      uint32_t x = 0;
+      const uint8_t* L = reinterpret_cast<const uint8_t*>(img + lw);
+      for (uint32_t i = 0; i < n; ++i) x |= src.byte(pos + k + i) ^ L[off + i];
+      if (x) {
+        sel = dead;
+        return len;
+      }
+      sel = img[t0 + (w >> 16)];
+      k += n;
+    }
+    return k;
   }
   __device__ __forceinline__ void step(const uint32_t* __restrict__ img, uint32_t b) {
     uint32_t s = (sel >> kLdsRowShift) + b;
@@ -199,11 +257,32 @@ struct LdsChain {
     sel = (e & 0xffu) == b ? e : dead;
   }
   __device__ __forceinline__ bool dead_now() const { return sel == dead; }
-  // continue the walk over bytes [k, len) of the field at pos
+  // continue the walk over bytes [k, len) of the field at pos; rows with
+  // skip descriptors are handled at 8-byte block boundaries
   template <class Src>
   __device__ __forceinline__ void run(const uint32_t* __restrict__ img, const Src& src, uint32_t pos, uint32_t len,
                                       uint32_t k) {
 #define L7M_STEP(B) step(img, (B));
+    if (slim != ~0u) {
+      while (k + 8 <= len) {
+        const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
+        const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
+        const uint32_t b4 = src.byte(pos + k + 4), b5 = src.byte(pos + k + 5);
+        const uint32_t b6 = src.byte(pos + k + 6), b7 = src.byte(pos + k + 7);
+        L7M_STEP(b0)
+        L7M_STEP(b1)
+        L7M_STEP(b2)
+        L7M_STEP(b3)
+        L7M_STEP(b4)
+        L7M_STEP(b5)
+        L7M_STEP(b6)
+        L7M_STEP(b7)
+        k += 8;
+        if (dead_now()) return;
+        if ((sel >> kLdsRowShift) >= slim) k = skip(img, src, pos, len, k);
+      }
+      if (dead_now()) return;
+    }
     L7M_WALK_BYTES(L7M_STEP, dead_now())
 #undef L7M_STEP
   }

@@ -46,6 +46,10 @@ struct Span {
 // Every table has an HBM copy in the program; the hot ones are also part of
 // the LDS image (lds_* != kNone), where es/latch are stored as u16 (0xffff =
 // latched accept / none).
+// Skip descriptor kinds (dfa_pack.h PackedDfa::skip, DfaDesc::lds_skip).
+constexpr uint32_t kSkipLoop = 1u, kSkipLit = 2u;
+constexpr uint32_t kSkipMaxLit = 31, kSkipMaxPool = 512, kSkipMaxRows = 1024;
+
 struct DfaDesc {
   uint32_t table_off;    // program: u32 T[n_slots]
   uint32_t es_off;       // program: u32 es[n_slots]
@@ -70,7 +74,10 @@ struct DfaDesc {
   uint32_t start_es8;    // lds_es == kLdsEsInEntry: the start state's end code (es8)
   uint32_t lit_tab;      // program: u32 pairs per local pattern {word offset, length} of its
                          // literal value (kNone: not a literal), or kNone (HBM-walked DFAs only)
-  uint32_t pad[2];
+  uint32_t lds_skip;     // LDS image word offset of the skip descriptors (dfa_pack.h kSkip*,
+                         // one word per base >= skip_lim), or kNone (LDS-walked DFAs only)
+  uint32_t skip_lim;     // skip rows: bases >= skip_lim (low 16 bits); the literal pool
+                         // (skip_lim >> 16 words) sits right below lds_skip
 };
 static_assert(sizeof(DfaDesc) == 96, "dfa desc is 24 words");
 

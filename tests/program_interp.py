@@ -23,7 +23,9 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi "
               "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
-              "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab").split()
+              "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab "
+              "lds_skip skip_lim").split()
+SKIP_LOOP, SKIP_LIT = 1, 2  # program.h kSkipLoop / kSkipLit
 ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 
 
@@ -43,7 +45,8 @@ def name_hash(data: bytes) -> int:
 
 
 class HttpProgram:
-    def __init__(self, prog: np.ndarray):
+    def __init__(self, prog: np.ndarray, skips: bool = True):
+        self.skips = skips  # follow the kernel's skip rows (dfa_pack.h) at 8-byte block boundaries
         self.w = prog.astype(np.uint64).astype(np.int64).tolist()
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
         h = self.h
@@ -89,14 +92,58 @@ class HttpProgram:
             # LDS copy (program.h kLdsRowShift): e = (image row index << 16) |
             # es8 << 8 | label, the table's row 0 is the dead row
             t0 = d["lds_table"]
-            for b in data:
-                if not base:
-                    break
-                slot = base + b
+            slim = (d["skip_lim"] & 0xFFFF) if (self.skips and d["lds_skip"] != KNONE) else None
+            n = len(data)
+            st = [base, es8, last]
+
+            def step(c):
+                bs = st[0]
+                slot = bs + c
                 e = self.img[t0 + slot]
-                if base < d["region"]:
-                    last = slot
-                base, es8 = ((e >> 16) - t0, (e >> 8) & 0xFF) if (e & 0xFF) == b else (0, 0)
+                if bs < d["region"]:
+                    st[2] = slot
+                st[0], st[1] = ((e >> 16) - t0, (e >> 8) & 0xFF) if (e & 0xFF) == c else (0, 0)
+
+            def skip(k):  # l7m_kernels.hip LdsChain::skip
+                for _ in range(64):
+                    bs = st[0]
+                    if bs < slim or not bs or k >= n:
+                        return k
+                    sk = d["lds_skip"]
+                    w = self.img[sk + bs - slim]
+                    if w & SKIP_LOOP:
+                        if any((self.img[t0 + bs + c] & 0xFF) != c for c in data[k:]):
+                            st[0] = 0
+                        return n
+                    if not (w & SKIP_LIT):
+                        return k
+                    ln, off, tslot = (w >> 2) & 31, (w >> 7) & 511, w >> 16
+                    if n - k < ln:
+                        st[0] = 0
+                        return n
+                    lw = sk - (d["skip_lim"] >> 16)
+                    pool = b"".join(int(x).to_bytes(4, "little") for x in self.img[lw:sk])
+                    if data[k:k + ln] != pool[off:off + ln]:
+                        st[0] = 0
+                        return n
+                    e = self.img[t0 + tslot]
+                    st[0], st[1] = (e >> 16) - t0, (e >> 8) & 0xFF
+                    k += ln
+                return k
+
+            k = 0
+            if base and slim is not None:
+                while k + 8 <= n and st[0]:
+                    for c in data[k:k + 8]:
+                        if st[0]:
+                            step(c)
+                    k += 8
+                    if st[0] and st[0] >= slim:
+                        k = skip(k)
+            while k < n and st[0]:
+                step(data[k])
+                k += 1
+            base, es8, last = st
         else:
             for b in data:
                 if not base:
