@@ -216,14 +216,7 @@ struct LdsChain {
       const uint32_t w = img[sk + (row - slim)];
       if (w & kSkipLoop) {  // every byte must be one of the row's own labels
         uint32_t bad = 0;
-        for (; k + 4 <= len; k += 4) {
-          const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
-          const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
-          bad |= (img[row + b0] ^ b0) & 0xffu;
-          bad |= (img[row + b1] ^ b1) & 0xffu;
-          bad |= (img[row + b2] ^ b2) & 0xffu;
-          bad |= (img[row + b3] ^ b3) & 0xffu;
-        }
+#pragma nounroll
         for (; k < len; ++k) {
           const uint32_t b = src.byte(pos + k);
           bad |= (img[row + b] ^ b) & 0xffu;
@@ -239,6 +232,7 @@ struct LdsChain {
       }
       uint32_t x = 0;
       const uint8_t* L = reinterpret_cast<const uint8_t*>(img + lw);
+#pragma nounroll
       for (uint32_t i = 0; i < n; ++i) x |= src.byte(pos + k + i) ^ L[off + i];
       if (x) {
         sel = dead;
@@ -263,27 +257,45 @@ struct LdsChain {
   __device__ __forceinline__ void run(const uint32_t* __restrict__ img, const Src& src, uint32_t pos, uint32_t len,
                                       uint32_t k) {
 #define L7M_STEP(B) step(img, (B));
-    if (slim != ~0u) {
-      while (k + 8 <= len) {
-        const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
-        const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
-        const uint32_t b4 = src.byte(pos + k + 4), b5 = src.byte(pos + k + 5);
-        const uint32_t b6 = src.byte(pos + k + 6), b7 = src.byte(pos + k + 7);
-        L7M_STEP(b0)
-        L7M_STEP(b1)
-        L7M_STEP(b2)
-        L7M_STEP(b3)
-        L7M_STEP(b4)
-        L7M_STEP(b5)
-        L7M_STEP(b6)
-        L7M_STEP(b7)
-        k += 8;
-        if (dead_now()) return;
-        if ((sel >> kLdsRowShift) >= slim) k = skip(img, src, pos, len, k);
-      }
+    // 8-byte blocks (the dead state is absorbing: one exit test per block);
+    // a row with a skip descriptor is handled at the block boundary (slim =
+    // ~0u without descriptors: never)
+    while (k + 8 <= len) {
+      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
+      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
+      const uint32_t b4 = src.byte(pos + k + 4), b5 = src.byte(pos + k + 5);
+      const uint32_t b6 = src.byte(pos + k + 6), b7 = src.byte(pos + k + 7);
+      L7M_STEP(b0)
+      L7M_STEP(b1)
+      L7M_STEP(b2)
+      L7M_STEP(b3)
+      L7M_STEP(b4)
+      L7M_STEP(b5)
+      L7M_STEP(b6)
+      L7M_STEP(b7)
+      k += 8;
       if (dead_now()) return;
+#ifndef L7M_NO_SKIP
+      if constexpr (Src::kLds)  // staged records (HBM-direct ones walk every byte: less code)
+        if ((sel >> kLdsRowShift) >= slim) k = skip(img, src, pos, len, k);
+#endif
     }
-    L7M_WALK_BYTES(L7M_STEP, dead_now())
+    if (k + 4 <= len && !dead_now()) {  // then at most one 4-byte block
+      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
+      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
+      L7M_STEP(b0)
+      L7M_STEP(b1)
+      L7M_STEP(b2)
+      L7M_STEP(b3)
+      k += 4;
+    }
+    if (k < len && !dead_now()) {  // the last 1-3 bytes, no loop
+      L7M_STEP(src.byte(pos + k))
+      if (k + 1 < len) {
+        L7M_STEP(src.byte(pos + k + 1))
+        if (k + 2 < len) L7M_STEP(src.byte(pos + k + 2))
+      }
+    }
 #undef L7M_STEP
   }
   __device__ __forceinline__ uint32_t code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
