@@ -67,10 +67,107 @@ struct FieldPattern {
   }
 };
 
+// Search automaton of <= kSearchMaxPats RE2-dialect patterns (program.h
+// kDfaSearch): the dense DFA of [\x00-\xff]*(p0|...|pk) with, per state, the
+// patterns matching a substring that ends there (mid set, '$' unsatisfied)
+// and at the end of the input (end set).
+struct SearchDfa {
+  uint32_t nstates = 0, ncls = 0, start = 0, start_mid = 0;
+  uint8_t cmap[256] = {0};
+  std::vector<uint32_t> table;    // nstates * ncls: next state | mid id << 24
+  std::vector<uint32_t> endmask;  // per state
+  std::vector<uint32_t> midmask;  // per mid id (0: no pattern)
+};
+
+re::Status build_search_dfa(const std::vector<const re::Ast*>& pats, SearchDfa* out) {
+  if (pats.size() > kSearchMaxPats) return re::Status::TooBig;
+  std::vector<re::Ast> a(pats.size());
+  std::vector<const re::Ast*> ptrs;
+  for (size_t i = 0; i < pats.size(); ++i) {
+    a[i] = *pats[i];
+    re::simplify_search(&a[i]);
+    re::make_search_prefix(&a[i]);
+    ptrs.push_back(&a[i]);
+  }
+  re::Dfa d;
+  re::DfaLimits lim;
+  lim.max_states = 1u << 17;
+  lim.max_table_bytes = 32ull << 20;
+  const re::Status st = re::build_dfa(ptrs, lim, &d, /*with_mid=*/true);
+  if (st != re::Status::Ok) return st;
+  if (static_cast<uint64_t>(d.nstates) * d.ncls >= (1u << 24)) return re::Status::TooBig;
+  std::vector<uint32_t> set_mask(d.sets.size(), 0);
+  for (size_t k = 0; k < d.sets.size(); ++k)
+    for (uint32_t p : d.sets[k]) set_mask[k] |= 1u << p;
+  // mid ids: distinct mid sets, 0 = the empty set
+  std::vector<uint32_t> mid_id(d.sets.size(), kNone);
+  out->midmask.assign(1, 0u);
+  mid_id[0] = 0;
+  for (int q = 0; q < d.nstates; ++q) {
+    const uint32_t sid = d.midset[q];
+    if (mid_id[sid] != kNone) continue;
+    if (out->midmask.size() >= kSearchMaxMid) return re::Status::TooBig;
+    mid_id[sid] = static_cast<uint32_t>(out->midmask.size());
+    out->midmask.push_back(set_mask[sid]);
+  }
+  out->nstates = static_cast<uint32_t>(d.nstates);
+  out->ncls = static_cast<uint32_t>(d.ncls);
+  out->start = static_cast<uint32_t>(d.start);
+  out->start_mid = set_mask[d.midset[d.start]];
+  std::memcpy(out->cmap, d.cmap, 256);
+  out->table.resize(static_cast<size_t>(d.nstates) * d.ncls);
+  for (size_t i = 0; i < out->table.size(); ++i) {
+    const uint32_t nx = d.next[i];
+    out->table[i] = nx | mid_id[d.midset[nx]] << 24;
+  }
+  out->endmask.resize(d.nstates);
+  for (int q = 0; q < d.nstates; ++q) out->endmask[q] = set_mask[d.endset[q]];
+  return re::Status::Ok;
+}
+
 struct Group {
   std::vector<uint32_t> pats;  // field pattern indices (local id = position)
-  PackedDfa pk;
+  PackedDfa pk;                // kDfaPacked groups
+  bool search = false;         // kDfaSearch group (sd)
+  SearchDfa sd;
 };
+
+// Search groups of one field's RE2-dialect patterns: chunks of
+// kSearchMaxPats, halved while an automaton exceeds the limits.
+int build_search_groups(const std::vector<const re::Ast*>& asts, std::vector<uint32_t> idx,
+                        std::vector<Group>* out, std::string* err) {
+  if (idx.size() > kSearchMaxPats) {
+    for (size_t o = 0; o < idx.size(); o += kSearchMaxPats) {
+      std::vector<uint32_t> part(idx.begin() + o, idx.begin() + std::min(idx.size(), o + kSearchMaxPats));
+      const int rc = build_search_groups(asts, std::move(part), out, err);
+      if (rc != L7M_OK) return rc;
+    }
+    return L7M_OK;
+  }
+  std::vector<const re::Ast*> sub;
+  for (uint32_t i : idx) sub.push_back(asts[i]);
+  Group g;
+  g.search = true;
+  const re::Status st = build_search_dfa(sub, &g.sd);
+  if (st == re::Status::Ok) {
+    g.pats = std::move(idx);
+    out->push_back(std::move(g));
+    return L7M_OK;
+  }
+  if (st != re::Status::TooBig) {
+    *err = "search DFA construction failed";
+    return L7M_EUNSUPPORTED;
+  }
+  if (idx.size() == 1) {
+    *err = "a single search pattern exceeds the DFA state limit";
+    return L7M_ETOOBIG;
+  }
+  const size_t h = idx.size() / 2;
+  std::vector<uint32_t> a(idx.begin(), idx.begin() + h), b(idx.begin() + h, idx.end());
+  const int rc = build_search_groups(asts, std::move(a), out, err);
+  if (rc != L7M_OK) return rc;
+  return build_search_groups(asts, std::move(b), out, err);
+}
 
 // Build the field automata of one field's patterns: normally ONE automaton
 // (dfa_pack.h, linear in the rules for prefix-diverging sets); a set whose
@@ -222,9 +319,6 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
 
   // 3. parse patterns and build DFA groups per field
   FieldDfaLimits lim;
-  // Unanchored-search automata of several patterns grow with the product of
-  // the patterns' progress states (no pattern ever dies); split early.
-  if (re2) lim.max_multi_states = 1u << 14;
   if (opts.max_dfa_states) lim.max_multi_states = opts.max_dfa_states;
   if (opts.max_table_bytes) lim.max_slots = std::min<uint64_t>(lim.max_slots, opts.max_table_bytes / 4);
   std::vector<std::vector<Group>> groups(nf);
@@ -245,7 +339,6 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
                                             " (regexp.Compile would fail)");
         if (st != re::Status::Ok)
           return fail(L7M_EUNSUPPORTED, "regex '" + fp.value + "': " + perr + " is outside the RE2 byte subset");
-        re::make_search(&asts[p]);
       } else if (fp.kind == MatchKind::Regex) {
         try {
           std::regex probe(fp.value, std::regex::ECMAScript | std::regex::optimize);
@@ -266,11 +359,20 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       }
       ptrs.push_back(&asts[p]);
     }
-    std::vector<uint32_t> idx(fpats[f].size());
-    for (uint32_t p = 0; p < idx.size(); ++p) idx[p] = p;
+    // RE2 dialect: regex patterns become search automata (program.h
+    // kDfaSearch); literal header values stay full-match packed automata
+    std::vector<uint32_t> idx, sidx;
+    for (uint32_t p = 0; p < fpats[f].size(); ++p)
+      (re2 && fpats[f][p].kind == MatchKind::Regex ? sidx : idx).push_back(p);
     std::string err;
-    int rc = build_groups(ptrs, idx, lim, &groups[f], &err);
-    if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+    if (!idx.empty()) {
+      int rc = build_groups(ptrs, idx, lim, &groups[f], &err);
+      if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+    }
+    if (!sidx.empty()) {
+      int rc = build_search_groups(ptrs, sidx, &groups[f], &err);
+      if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+    }
     fp_loc[f].assign(fpats[f].size(), {0, 0});
     for (uint32_t g = 0; g < groups[f].size(); ++g)
       for (uint32_t l = 0; l < groups[f][g].pats.size(); ++l)
@@ -429,7 +531,18 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     dd[k].lit_tab = kNone;
     dd[k].lds_skip = kNone;
     dd[k].skip_lim = 0;
-    total_states += d.nstates;
+    dd[k].kind = kDfaPacked;
+    if (all[k].grp && all[k].grp->search) {
+      const SearchDfa& sd = all[k].grp->sd;
+      dd[k].kind = kDfaSearch;
+      dd[k].start_base = sd.start;
+      dd[k].start_es8 = sd.start_mid;
+      dd[k].region = 0;
+      dd[k].n_slots = sd.nstates * sd.ncls;
+      dd[k].nstates = sd.nstates;
+      dd[k].acc_ncls = sd.ncls;
+    }
+    total_states += dd[k].nstates;
     for (size_t s = 0; s < d.sets.size(); ++s) {
       sets.push_back(push_list(d.sets[s]));
       if (k < ndfa) {
@@ -475,9 +588,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   // kHttpMinStage bytes per wave (l7m_kernels.hip http_lds_bytes).  What is
   // left bounds the table image; rule sets whose fixed part does not fit are
   // rejected here, when the policy loads, not on every batch.
-  const uint64_t codes_bytes = ndfa > kHttpRegDfas ? 4ull * kHttpBlock * ndfa : 0;
+  bool any_search = false;
+  for (uint32_t f = 0; f < nf; ++f)
+    for (const auto& g : groups[f]) any_search |= g.search;
+  // (search programs keep their end codes in a global scratch, l7m_kernels.hip)
+  const uint64_t codes_bytes = ndfa > kHttpRegDfas && !any_search ? 4ull * kHttpBlock * ndfa : 0;
   const uint64_t ctr_bytes = n + 2 <= kMaxLdsCounters ? 4ull * ((n + 2 + 3) & ~uint64_t(3)) : 0;
-  const uint64_t stage_bytes = static_cast<uint64_t>(kHttpWaves) * (kHttpMinStage + 16);
+  const uint64_t stage_bytes = static_cast<uint64_t>(kHttpWaves) * (kHttpMinStage + 16) + kHttpPrefetchSink;
   uint64_t img = 0;  // image words
   auto img_take = [&](uint64_t words) {
     uint64_t o = img;
@@ -544,6 +661,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   for (uint32_t k = 0; k < ndt; ++k) order[k] = k;
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hotness(a) < hotness(b); });
   for (uint32_t k : order) {
+    if (dd[k].kind == kDfaSearch) continue;  // search automata are walked from the program
     const PackedDfa& d = *all[k].d;
     const uint64_t half_es = (d.n_slots + 1) / 2, half_latch = (d.latch.size() + 1) / 2;
     const uint64_t need = ((d.n_slots + 3) & ~3ull) + ((half_es + 3) & ~3ull) + ((half_latch + 3) & ~3ull);
@@ -633,14 +751,23 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     h.pres_fields_hi = static_cast<uint32_t>(pm >> 32);
   }
   h.n_policies = plan.n_policies;
+  for (uint32_t k = 0; k < ndfa; ++k) h.search |= dd[k].kind == kDfaSearch ? 1u : 0u;
   h.ent_mask = ent_slots - 1;
   h.ent_tab_off = take(2ull * ent_slots);
   h.off_pool = take(pool.size());
   h.off_cr = take(cr.size());
   for (uint32_t k = 0; k < ndt; ++k) {
-    dd[k].table_off = take(all[k].d->n_slots);
-    dd[k].es_off = take(all[k].d->n_slots);
-    dd[k].latch_off = take(all[k].d->latch.size());
+    if (dd[k].kind == kDfaSearch) {
+      dd[k].table_off = take(dd[k].n_slots);
+      dd[k].es_off = take(dd[k].nstates);  // end masks
+      dd[k].latch_off = take(0);
+      dd[k].acc_cmap_off = take(256 / 4);
+      dd[k].acc_mid_off = take(kSearchMaxMid);
+    } else {
+      dd[k].table_off = take(all[k].d->n_slots);
+      dd[k].es_off = take(all[k].d->n_slots);
+      dd[k].latch_off = take(all[k].d->latch.size());
+    }
     w = (w + 15) & ~uint64_t(15);  // candidate entries on 64-byte boundaries
     dd[k].ct_off = take(16 * ct[k].size());
     dd[k].ctmask_off = take((ct[k].size() + 31) / 32);
@@ -688,9 +815,17 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   std::memcpy(P, &h, sizeof h);
   for (uint32_t k = 0; k < ndt; ++k) {
     const PackedDfa& d = *all[k].d;
-    std::memcpy(P + dd[k].table_off, d.table.data(), d.n_slots * 4ull);
-    std::memcpy(P + dd[k].es_off, d.es.data(), d.n_slots * 4ull);
-    std::memcpy(P + dd[k].latch_off, d.latch.data(), d.latch.size() * 4ull);
+    if (dd[k].kind == kDfaSearch) {
+      const SearchDfa& sd = all[k].grp->sd;
+      std::memcpy(P + dd[k].table_off, sd.table.data(), sd.table.size() * 4ull);
+      std::memcpy(P + dd[k].es_off, sd.endmask.data(), sd.endmask.size() * 4ull);
+      std::memcpy(P + dd[k].acc_cmap_off, sd.cmap, 256);
+      std::memcpy(P + dd[k].acc_mid_off, sd.midmask.data(), sd.midmask.size() * 4ull);
+    } else {
+      std::memcpy(P + dd[k].table_off, d.table.data(), d.n_slots * 4ull);
+      std::memcpy(P + dd[k].es_off, d.es.data(), d.n_slots * 4ull);
+      std::memcpy(P + dd[k].latch_off, d.latch.data(), d.latch.size() * 4ull);
+    }
     std::vector<CandEntry> ce(ct[k].size());
     std::memset(ce.data(), 0, ce.size() * sizeof(CandEntry));
     for (size_t i = 0; i < ct[k].size(); ++i) {

@@ -36,7 +36,26 @@ constexpr uint32_t kWaves = kHttpWaves;
 constexpr uint32_t kBlock = kHttpBlock;
 constexpr uint32_t kMaxStage = kHttpMaxStage;  // bytes of records staged per wave and tile
 constexpr uint32_t kCopyIters = kMaxStage / 1024;
+constexpr uint32_t kPrefetchSink = kHttpPrefetchSink;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Explicit address-space loads where one expression picks between an LDS
+// word and a program word: left generic, the compiler merges the two into a
+// flat load of a selected pointer, and a flat load waits for vmcnt(0) AND
+// lgkmcnt(0) -- i.e. for the next tile's bytes in flight.
+typedef __attribute__((address_space(1))) const uint32_t* gptr_u32;
+typedef __attribute__((address_space(3))) const uint32_t* lptr_u32;
+__device__ __forceinline__ uint32_t gld(const uint32_t* p) { return *(gptr_u32)(p); }
+__device__ __forceinline__ uint32_t lld(const uint32_t* p) { return *(lptr_u32)(p); }
+// A program load whose wait is placed right here (in the branch that needs
+// it): the verification phase runs after the next tile's bytes were
+// requested, and a wait the compiler puts at a later join would be vmcnt(0)
+// on every path through it, the common LDS-only one included.
+__device__ __forceinline__ uint32_t gld_now(const uint32_t* p) {
+  uint32_t v = gld(p);
+  asm volatile("" : "+v"(v));
+  return v;
+}
 
 // Where a record's bytes are read from.
 struct LdsSrc {
@@ -64,9 +83,9 @@ __device__ __forceinline__ uint32_t end_code(const uint32_t* __restrict__ img, c
     if (es != kEs16Latched) return es;
     return kLatchedBit | (last == kNone ? dd.start_latch : I16[dd.lds_latch + last]);
   }
-  const uint32_t es = prog[dd.es_off + base];
+  const uint32_t es = gld(prog + dd.es_off + base);
   if (es != kLatchedBit) return es;
-  return kLatchedBit | (last == kNone ? dd.start_latch : prog[dd.latch_off + last]);
+  return kLatchedBit | (last == kNone ? dd.start_latch : gld(prog + dd.latch_off + last));
 }
 
 // Walk `len` bytes at byte `pos` of the record through one packed DFA
@@ -155,8 +174,8 @@ __device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, c
     if (base && !lit_stop) L7M_WALK_BYTES(L7M_STEP, !base)
   }
   if (lit_stop) {
-    const uint32_t p = last == kNone ? dd.start_latch : prog[dd.latch_off + last];
-    const uint32_t lo = prog[dd.lit_tab + 2 * p], ll = prog[dd.lit_tab + 2 * p + 1];
+    const uint32_t p = last == kNone ? dd.start_latch : gld(prog + dd.latch_off + last);
+    const uint32_t lo = gld(prog + dd.lit_tab + 2 * p), ll = gld(prog + dd.lit_tab + 2 * p + 1);
     if (lo != kNone) {
       // bytes [0, k) followed the literal (the walk is latched on it): the
       // field matches iff it has the literal's length and the rest is equal
@@ -183,6 +202,8 @@ __device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, c
 //     slot = (sel >> 16) + b;  e = img[slot];  sel = label(e) == b ? e : dead
 // with the word / byte selects folded into SDWA operands.  `slast` is the
 // slot of the last transition taken from a multi-pattern row (below lim).
+constexpr uint32_t kSkipMinRest = 64;  // bytes left in the field for a skip descriptor to be taken
+
 struct LdsChain {
   uint32_t sel, dead, lim, slast;
   uint32_t slim;  // rows >= slim carry skip descriptors (dfa_pack.h), ~0u: none
@@ -276,8 +297,12 @@ struct LdsChain {
       k += 8;
       if (dead_now()) return;
 #ifndef L7M_NO_SKIP
-      if constexpr (Src::kLds)  // staged records (HBM-direct ones walk every byte: less code)
-        if ((sel >> kLdsRowShift) >= slim) k = skip(img, src, pos, len, k);
+      // staged records (HBM-direct ones walk every byte: less code), and only
+      // with a long rest: a lane in the skip handler runs its own loop while
+      // the wave's other lanes wait, which costs more than walking a short
+      // rest in step with them (config 2's `/api/w/.*` tails: 3.56 -> 4.62 ms)
+      if constexpr (Src::kLds)
+        if ((sel >> kLdsRowShift) >= slim && len - k >= kSkipMinRest) k = skip(img, src, pos, len, k);
 #endif
     }
     if (k + 4 <= len && !dead_now()) {  // then at most one 4-byte block
@@ -326,7 +351,7 @@ __device__ __forceinline__ uint32_t walk_lds(const uint32_t* __restrict__ img, c
 
 __device__ __forceinline__ bool set_has(const uint32_t* __restrict__ pool, Span s, uint32_t p) {
   for (uint32_t j = 0; j < s.len; ++j) {
-    const uint32_t v = pool[s.off + j];
+    const uint32_t v = gld_now(pool + s.off + j);
     if (v == p) return true;
     if (v > p) return false;  // sorted
   }
@@ -398,6 +423,27 @@ struct Codes<0> {
   __device__ __forceinline__ uint32_t get(uint32_t d) const { return p[d * kBlock]; }
 };
 
+// Programs with search automata (kReg = -1, RE2 dialect): one code word per
+// value DFA, dozens of DFAs, kept in a global scratch column per thread
+// (stride = the grid's threads); agent-scope loads and stores, so a later
+// tile never reads a stale line of an earlier one.
+template <>
+struct Codes<-1> {
+  uint32_t* p;
+  uint32_t stride;
+  __device__ __forceinline__ void clear(uint32_t n) {
+    for (uint32_t d = 0; d < n; ++d) __hip_atomic_store(p + d * stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ void set(uint32_t d, uint32_t v) {
+    __hip_atomic_store(p + d * stride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ uint32_t get(uint32_t d) const {
+    uint32_t v = __hip_atomic_load(p + d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" : "+v"(v));
+    return v;
+  }
+};
+
 struct Ctx {
   const uint32_t* prog;
   const uint32_t* img;         // LDS image
@@ -410,9 +456,29 @@ struct Ctx {
   const Span* remotes;         // HBM
 };
 
-template <bool kLit, class Src>
+// Search automaton (program.h kDfaSearch, RE2 dialect): the mask of the
+// patterns matching some substring of the field -- per byte one dependent
+// table read, and the mask of the patterns whose match ends there.
+template <class Src>
+__device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd, const Src& src, uint32_t pos,
+                                                uint32_t len) {
+  const uint32_t* __restrict__ T = c.prog + dd.table_off;
+  const uint8_t* __restrict__ cm = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
+  const uint32_t* __restrict__ mid = c.prog + dd.acc_mid_off;
+  const uint32_t ncls = dd.acc_ncls;
+  uint32_t st = dd.start_base, acc = dd.start_es8;
+  for (uint32_t k = 0; k < len; ++k) {
+    const uint32_t e = gld(T + st * ncls + cm[src.byte(pos + k)]);
+    st = e & 0xffffffu;
+    acc |= gld(mid + (e >> 24));
+  }
+  return acc | gld(c.prog + dd.es_off + st);
+}
+
+template <bool kLit, bool kSearch, class Src>
 __device__ __forceinline__ uint32_t walk_dfa(const Ctx& c, uint32_t d, const Src& src, uint32_t pos, uint32_t len) {
   const DfaDesc& dd = c.dds[d];
+  if (kSearch && dd.kind == kDfaSearch) return walk_search(c, dd, src, pos, len);
   if (dd.lds_table != kNone) return walk_lds(c.img, c.prog, dd, src, pos, len);
   return walk_hbm<kLit>(c.img, c.prog, dd, src, pos, len);
 }
@@ -463,24 +529,28 @@ __device__ __forceinline__ uint32_t name_field_of(const Ctx& c, const HttpHeader
 }
 
 // Does end code `code` of DFA d contain pattern p?
+template <bool kSearch>
 __device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code, uint32_t p) {
   if (code == 0) return false;
-  if (code & kLatchedBit) return (code & ~kLatchedBit) == p;
   const DfaDesc& dd = c.dds[d];
+  if (kSearch && dd.kind == kDfaSearch) return ((code >> p) & 1u) != 0;  // code = matched-pattern mask
+  if (code & kLatchedBit) return (code & ~kLatchedBit) == p;
   if (dd.lds_mask != kNone) {
     const uint32_t* m = c.img + dd.lds_mask + 2u * code;
     return ((p < 32 ? m[0] >> p : m[1] >> (p - 32)) & 1u) != 0;
   }
-  return set_has(c.pool, c.sets[dd.set_base + code], p);
+  const uint32_t* sp = reinterpret_cast<const uint32_t*>(c.sets + dd.set_base + code);
+  return set_has(c.pool, Span{gld_now(sp), gld_now(sp + 1)}, p);
 }
 
 // (policy, direction, port) -> entry | kEntHaveHttp, or kNone (program.h).
 __device__ __forceinline__ uint32_t ent_lookup(const Ctx& c, const HttpHeader& h, uint32_t key) {
-  const uint32_t* tab = h.lds_ent_tab != kNone ? c.img + h.lds_ent_tab : c.prog + h.ent_tab_off;
+  const bool lds = h.lds_ent_tab != kNone;
+  const uint32_t* tab = lds ? c.img + h.lds_ent_tab : c.prog + h.ent_tab_off;
   for (uint32_t at = ent_hash(key) & h.ent_mask;; at = (at + 1) & h.ent_mask) {
-    const uint32_t k = tab[2 * at];
+    const uint32_t k = lds ? lld(tab + 2 * at) : gld(tab + 2 * at);
     if (k == 0) return kNone;
-    if (k == key + 1) return tab[2 * at + 1];
+    if (k == key + 1) return lds ? lld(tab + 2 * at + 1) : gld(tab + 2 * at + 1);
   }
 }
 
@@ -512,7 +582,9 @@ struct WalkOut {
   uint64_t present;   // fields present in the request
   uint32_t ex, e0;    // port entries whose rules may decide (exact port, port 0)
   uint32_t remote;    // the request's remote identity
-  uint32_t pf_t;      // the candidate-entry touch (kept live until verification)
+  uint32_t pf_t;      // the candidate-entry touch (kept live until the entry load)
+  uint32_t pf_d;      // DFA whose candidate entry was touched, or kNone
+  uint32_t pf_ent;    // that entry's word offset in the program, or kNone
   bool h0;            // the port-0 entry has HTTP rules
 };
 constexpr int32_t kNeedVerify = INT32_MIN;
@@ -587,14 +659,14 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
   // is touched (one dword load) as soon as that walk ends, so its L2 round
   // trip overlaps the remaining walks and verification reads the entry from
   // the CU's L1 (the walks in between touch no global memory).
-  uint32_t pf_d = kNone, pf_t = 0;
-  (void)pf_d;
+  uint32_t pf_d = kNone, pf_t = 0, pf_ent = kNone;
   auto touch = [&](uint32_t d, uint32_t code) {
     if (pf_d == kNone && code && ((cand_all >> d) & 1ull)) {
       const DfaDesc& dd = c.dds[d];
-      if (dd.lds_ct == kNone) {
+      if (dd.lds_ct == kNone && !(kReg < 0 && dd.kind == kDfaSearch)) {
         const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
-        pf_t = c.prog[dd.ct_off + 16u * idx];
+        pf_ent = dd.ct_off + 16u * idx;
+        pf_t = c.prog[pf_ent];
         pf_d = d;
       }
     }
@@ -620,7 +692,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         if (h.lds_name_tab != kNone) {
           f = name_field_of(c, h, src, hp, nl);
         } else {
-          const uint32_t code = walk_dfa<false>(c, h.n_dfas, src, hp, nl);
+          const uint32_t code = walk_dfa<false, false>(c, h.n_dfas, src, hp, nl);
           if (code & kLatchedBit) f = 3u + (code & ~kLatchedBit);
           else if (code) f = c.name_field[code];
         }
@@ -636,7 +708,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
       const FieldDesc& fd = c.fields[f];
       for (uint32_t k = 0; k < fd.ndfa; ++k) {
         const uint32_t d = fd.dfa_first + k;
-        const uint32_t code = walk_dfa<kLit>(c, d, src, p, len);
+        const uint32_t code = walk_dfa<kLit, (kReg < 0)>(c, d, src, p, len);
         codes.set(d, code);
         touch(d, code);
       }
@@ -655,14 +727,20 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
   o.h0 = h0;
   o.remote = w1;
   o.pf_t = pf_t;
+  o.pf_d = pf_d;
+  o.pf_ent = pf_ent;
   return kNeedVerify;
 }
 
 // Verification phase: the first rule (smallest index) among the keyed
 // candidates whose other matchers, port entry and remote set hold; the
 // check-record lists are selected by the walks' end codes.
+// `pe` holds the first 48 bytes of the candidate entry the walk phase touched
+// (o.pf_d), loaded before the next tile's bytes were requested: vmcnt counts
+// loads in issue order, so an entry load issued here would wait for them.
 template <int kReg>
-__device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o) {
+__device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o,
+                                               const u32x4 (&pe)[3]) {
   const Codes<kReg>& codes = o.codes;
   const uint64_t present = o.present;
   const uint32_t ex = o.ex, e0 = o.e0, remote = o.remote;
@@ -676,14 +754,16 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
   const uint64_t cand_all = masked ? ((static_cast<uint64_t>(h.cand_dfas_hi) << 32) | h.cand_dfas_lo) : 0;
   uint32_t best = h.always_rule;
   auto remote_ok = [&](uint32_t rid) -> bool {  // PortNetworkPolicyRule::Matches (h:92-97)
-    const Span rr = c.remotes[rid];
-    uint32_t lo = 0, hi = rr.len;
+    const uint32_t* rp = reinterpret_cast<const uint32_t*>(c.remotes + rid);
+    uint32_t roff = gld(rp), rlen = gld(rp + 1);
+    asm volatile("" : "+v"(roff), "+v"(rlen));
+    uint32_t lo = 0, hi = rlen;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (c.pool[rr.off + mid] < remote) lo = mid + 1;
+      if (gld_now(c.pool + roff + mid) < remote) lo = mid + 1;
       else hi = mid;
     }
-    return lo < rr.len && c.pool[rr.off + lo] == remote;
+    return lo < rlen && gld_now(c.pool + roff + lo) == remote;
   };
   auto scan = [&](Span cl) {
     uint32_t o = cl.off;
@@ -691,16 +771,18 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
       // one record: rid, header, up to 3 matchers fetched together
       uint32_t rw[8];
 #pragma unroll
-      for (uint32_t q = 0; q < 8; ++q) rw[q] = c.cr[o + q];
+      for (uint32_t q = 0; q < 8; ++q) rw[q] = gld(c.cr + o + q);
+      asm volatile("" : "+v"(rw[0]), "+v"(rw[1]), "+v"(rw[2]), "+v"(rw[3]), "+v"(rw[4]), "+v"(rw[5]), "+v"(rw[6]),
+                   "+v"(rw[7]));
       const uint32_t rid = rw[0], nm = cr_matchers(rw[1]);
       if (rid >= best) break;
       bool ok = eligible(rw[1]) && (!(rw[1] & kCrRemote) || remote_ok(rid));
       for (uint32_t q = 0; q < nm && ok; ++q) {
-        const uint32_t a = q < 3 ? (q == 0 ? rw[2] : q == 1 ? rw[4] : rw[6]) : c.cr[o + 2 + 2 * q];
-        const uint32_t pat = q < 3 ? (q == 0 ? rw[3] : q == 1 ? rw[5] : rw[7]) : c.cr[o + 3 + 2 * q];
+        const uint32_t a = q < 3 ? (q == 0 ? rw[2] : q == 1 ? rw[4] : rw[6]) : gld_now(c.cr + o + 2 + 2 * q);
+        const uint32_t pat = q < 3 ? (q == 0 ? rw[3] : q == 1 ? rw[5] : rw[7]) : gld_now(c.cr + o + 3 + 2 * q);
         const uint32_t f = a & 0xffu;
         if (!((present >> f) & 1ull)) ok = false;
-        else if (!((a >> 8) & 1u)) ok = code_has(c, a >> 9, codes.get(a >> 9), pat);
+        else if (!((a >> 8) & 1u)) ok = code_has<(kReg < 0)>(c, a >> 9, codes.get(a >> 9), pat);
       }
       if (ok) {
         best = rid;
@@ -722,7 +804,7 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
         if (q < nm && ok) {
           const uint32_t a = ma[q];
           if (!((present >> (a & 0xffu)) & 1ull)) ok = false;
-          else if (!((a >> 8) & 1u)) ok = code_has(c, a >> 9, codes.get(a >> 9), mp[q]);
+          else if (!((a >> 8) & 1u)) ok = code_has<(kReg < 0)>(c, a >> 9, codes.get(a >> 9), mp[q]);
         }
       }
       if (ok) best = rid;
@@ -730,11 +812,10 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
       scan(Span{q0.y, len});
     }
   };
-  auto check_inline = [&](const uint32_t* e) {  // e -> CandEntry (LDS or HBM)
+  auto check_inline = [&](const uint32_t* e) {  // e -> CandEntry in LDS
     const u32x4* q = reinterpret_cast<const u32x4*>(e);
     check_entry(q[0], q[1], q[2]);
   };
-  asm volatile("" ::"v"(o.pf_t));  // the touch completes here, not at its first use
   // only DFAs with candidate entries
   uint64_t cm = cand_all;
   for (uint32_t i = 0; masked ? cm != 0 : i < h.n_dfas; ++i) {
@@ -746,13 +827,38 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
     const uint32_t code = codes.get(d);
     if (!code) continue;
     const DfaDesc& dd = c.dds[d];
+    if (kReg < 0 && dd.kind == kDfaSearch) {  // candidates of every matched pattern (entry p)
+      for (uint32_t m = code; m; m &= m - 1) {
+        const uint32_t idx = static_cast<uint32_t>(__builtin_ctz(m));
+        const uint32_t mw = dd.lds_ctmask != kNone ? lld(c.img + dd.lds_ctmask + (idx >> 5))
+                                                   : gld_now(c.prog + dd.ctmask_off + (idx >> 5));
+        if (!((mw >> (idx & 31u)) & 1u)) continue;
+        if (dd.lds_ct != kNone) {
+          check_inline(c.img + dd.lds_ct + 16u * idx);
+        } else {
+          typedef __attribute__((address_space(1))) const u32x4* gq;
+          const gq q = (gq)(c.prog + dd.ct_off + 16u * idx);
+          u32x4 q0 = q[0], q1 = q[1], q2 = q[2];
+          asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2));
+          check_entry(q0, q1, q2);
+        }
+      }
+      continue;
+    }
     const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
-    const uint32_t mw = dd.lds_ctmask != kNone ? c.img[dd.lds_ctmask + (idx >> 5)] : c.prog[dd.ctmask_off + (idx >> 5)];
+    const uint32_t mw =
+        dd.lds_ctmask != kNone ? lld(c.img + dd.lds_ctmask + (idx >> 5)) : gld(c.prog + dd.ctmask_off + (idx >> 5));
     if (!((mw >> (idx & 31u)) & 1u)) continue;  // no candidates
     if (dd.lds_ct != kNone) {
       check_inline(c.img + dd.lds_ct + 16u * idx);
-    } else {
-      check_inline(c.prog + dd.ct_off + 16u * idx);
+    } else if (d == o.pf_d) {
+      check_entry(pe[0], pe[1], pe[2]);
+    } else {  // a further HBM candidate entry (not prefetched)
+      typedef __attribute__((address_space(1))) const u32x4* gq;
+      const gq q = (gq)(c.prog + dd.ct_off + 16u * idx);
+      u32x4 q0 = q[0], q1 = q[1], q2 = q[2];
+      asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2));
+      check_entry(q0, q1, q2);
     }
   }
   for (uint64_t pm = ((static_cast<uint64_t>(h.pres_fields_hi) << 32) | h.pres_fields_lo) & present; pm;
@@ -790,7 +896,8 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
                                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                            const uint64_t* __restrict__ offs, uint64_t n,
                                                            int32_t* __restrict__ verdicts,
-                                                           unsigned long long* __restrict__ hits, uint32_t stage) {
+                                                           unsigned long long* __restrict__ hits, uint32_t stage,
+                                                           uint32_t* __restrict__ scratch) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -798,7 +905,9 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
   const uint32_t n_ctr = h.n_rules + 2;
   uint32_t* ctr = smem + h.lds_image_words;  // LDS hit counters (kLdsHits)
   uint32_t* col = ctr + (kHits == kLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);  // LDS code columns (!kReg)
-  uint8_t* stg = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock)) + wv * (stage + 16u);
+  // pfz: the workgroup's 256-byte sink of the L2 prefetch (never read)
+  uint8_t* pfz = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock));
+  uint8_t* stg = pfz + kPrefetchSink + wv * (stage + 16u);
   {
     const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
     uint4* l = reinterpret_cast<uint4*>(img);
@@ -822,6 +931,29 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
 #ifdef L7M_PROF
   uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t prof_tile = 0;
+  // wave timeline per tile (s_memtime): [0] top wait, [1] walks, [2] entry
+  // wait, [3] issue, [4] verify + store, [5] counters; [6] tiles
+  uint64_t qt[7] = {0, 0, 0, 0, 0, 0, 0}, qlast = __builtin_amdgcn_s_memtime();
+#define QT(i)                                              \
+  do {                                                     \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
+    qt[i] += t_ - qlast;                                   \
+    qlast = t_;                                            \
+  } while (0)
+#define QTN(i)                                             \
+  do {                                                     \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
+    qt[i] += t_ - qlast;                                   \
+    qlast = t_;                                            \
+  } while (0)
+#else
+#define QT(i) \
+  do {        \
+  } while (0)
+#define QTN(i) QT(i)
 #endif
 
   // This wave's contiguous share of the batch, consumed in tiles of <= 64
@@ -910,6 +1042,21 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
 #endif
     wave_sync();
+    QTN(0);
+#ifdef L7M_L2PF
+    // The next tile's window is pulled into L2 now, while this tile is
+    // walked (one 4-byte LDS-DMA per 128-byte line, into the sink), so its
+    // LDS-DMA copy after the walks waits for L2 instead of HBM: a wave holds
+    // one stage, so the copy itself cannot be issued before the walks.
+    {
+      const Tile tp = plan(t.cur + t.take, o2, n2);
+      if (lane * 128u < tp.bytes)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(arena + tp.base + lane * 128u),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(pfz)),
+                                         4, 0, 0);
+    }
+#endif
 
     const uint64_t o = t.o, onext = t.onext, base = t.base;
     const uint32_t k = t.k, take = t.take;
@@ -919,6 +1066,10 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
 #endif
     WalkOut<kReg> wo;
     if constexpr (!kReg) wo.codes.p = mycol;
+    if constexpr (kReg < 0) {  // search programs: the codes live in the global scratch
+      wo.codes.p = scratch + static_cast<uint64_t>(blockIdx.x) * kBlock + tid;
+      wo.codes.stride = gridDim.x * kBlock;
+    }
     if (lane < take) {
       bool done = false;
       if (lane < k && onext - o >= L7M_HTTP_REC_FIXED) {
@@ -935,16 +1086,33 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
         v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
       }
     }
+    // The candidate entry the walks touched is loaded (an L1/L2 hit by now)
+    // and waited for BEFORE the next tile's bytes are requested: vmcnt is
+    // in-order, so verification reading it later would wait for the whole
+    // next tile from HBM.
+    QTN(1);
+    u32x4 pe[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    if (lane < take && v == kNeedVerify && wo.pf_ent != kNone) {
+      asm volatile("" ::"v"(wo.pf_t));  // the touch completes here, not at its first use
+      const u32x4* e = reinterpret_cast<const u32x4*>(c.prog + wo.pf_ent);
+      pe[0] = e[0];
+      pe[1] = e[1];
+      pe[2] = e[2];
+    }
+    asm volatile("" : "+v"(pe[0]), "+v"(pe[1]), "+v"(pe[2]));  // landed here
+    QTN(2);
     // The next tile's bytes are requested only now, after the walks: they
     // land during verification without holding kCopyIters x 4 registers
     // through the walks (the walks read LDS only).
     const Tile t2 = plan(t.cur + t.take, o2, n2);
     issue_bytes(t2);
     load_offs(t2.cur + t2.take, &o2, &n2);
+    QTN(3);
     if (lane < take) {
-      if (v == kNeedVerify) v = eval_verify<kReg>(c, h, wo);
+      if (v == kNeedVerify) v = eval_verify<kReg>(c, h, wo, pe);
       verdicts[t.cur + lane] = v;
     }
+    QTN(4);
 #ifdef L7M_PROF
     prof_tile += __builtin_amdgcn_s_memtime() - te0;
 #endif
@@ -961,9 +1129,20 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
     }
     wave_sync();  // the stage is overwritten by the next tile
     t = t2;
+    QTN(5);
+#ifdef L7M_PROF
+    qt[6] += 1;
+#endif
   }
 #ifdef L7M_PROF
-  if (blockIdx.x == 0 && wv == 0) {
+  if ((blockIdx.x == 0 && wv == 0) || (blockIdx.x == 101 && wv == 7)) {
+    if (lane == 0)
+      printf("L7M_QT block %u wave %u tiles %llu cycles/tile: topwait %llu walks %llu entry %llu issue %llu "
+             "verify %llu counters %llu\n",
+             blockIdx.x, wv, (unsigned long long)qt[6], (unsigned long long)(qt[0] / (qt[6] ? qt[6] : 1)),
+             (unsigned long long)(qt[1] / (qt[6] ? qt[6] : 1)), (unsigned long long)(qt[2] / (qt[6] ? qt[6] : 1)),
+             (unsigned long long)(qt[3] / (qt[6] ? qt[6] : 1)), (unsigned long long)(qt[4] / (qt[6] ? qt[6] : 1)),
+             (unsigned long long)(qt[5] / (qt[6] ? qt[6] : 1)));
     prof[7] = prof_tile;
     for (int q = 1; q < 8; ++q)
       for (uint32_t m = 1; m < 64; m <<= 1) {
@@ -987,10 +1166,10 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
 }  // namespace
 
 size_t http_lds_bytes(const HttpHeader& h, uint32_t stage) {
-  const bool reg = h.n_dfas <= kRegDfas;
+  const bool reg = h.n_dfas <= kRegDfas || h.search;  // search programs: codes in global scratch
   const size_t ctr = h.n_rules + 2 <= kMaxLdsCounters ? ((h.n_rules + 2 + 3) & ~size_t(3)) : 0;
   return 4u * (static_cast<size_t>(h.lds_image_words) + ctr + (reg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock)) +
-         static_cast<size_t>(kWaves) * (stage + 16u);
+         kPrefetchSink + static_cast<size_t>(kWaves) * (stage + 16u);
 }
 
 // Bytes of records staged per wave: what is left of the LDS after the tables.
@@ -1005,14 +1184,14 @@ uint32_t http_stage_bytes(const HttpHeader& h) {
 template <int kHits, int kReg, int kAblate = 0, bool kLit = false>
 static hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                       unsigned long long* hits, uint32_t stage) {
+                       unsigned long long* hits, uint32_t stage, uint32_t* scratch = nullptr) {
   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU); set per device
   // and instantiation, thread-safely (l7m_device.h)
   const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate, kLit>),
                                          kLdsBytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate, kLit>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
-                     offs, n, verdicts, hits, stage);
+                     offs, n, verdicts, hits, stage, scratch);
   return hipGetLastError();
 }
 
@@ -1036,6 +1215,23 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
     return launch_one<kNoHits, 8, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
   }
   const int mode = !hits ? kNoHits : (h.n_rules + 2 <= kMaxLdsCounters ? kLdsHits : kGlobalHits);
+  if (h.search) {
+    // RE2-dialect programs (search automata, program.h kDfaSearch): their own
+    // instantiation, end codes in a stream-ordered global scratch column per
+    // thread (n_dfas words each)
+    uint32_t* scratch = nullptr;
+    const size_t bytes = static_cast<size_t>(h.n_dfas ? h.n_dfas : 1) * grid.x * kBlock * 4u;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&scratch), bytes, stream);
+    if (e != hipSuccess) return e;
+    if (mode == kNoHits) e = launch_one<kNoHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts,
+                                                     hits, stage, scratch);
+    else if (mode == kLdsHits) e = launch_one<kLdsHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n,
+                                                            verdicts, hits, stage, scratch);
+    else e = launch_one<kGlobalHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage,
+                                         scratch);
+    const hipError_t e2 = hipFreeAsync(scratch, stream);
+    return e != hipSuccess ? e : e2;
+  }
   // end codes in 4 or 8 registers, or in LDS columns
   const bool lit = (flags & kLaunchLiterals) != 0;
 #define L7M_LAUNCH(M, R)                                                                                         \

@@ -78,8 +78,24 @@ struct DfaDesc {
                          // one word per base >= skip_lim), or kNone (LDS-walked DFAs only)
   uint32_t skip_lim;     // skip rows: bases >= skip_lim (low 16 bits); the literal pool
                          // (skip_lim >> 16 words) sits right below lds_skip
+  uint32_t kind;         // kDfaPacked, or kDfaSearch (below)
+  uint32_t acc_cmap_off; // kDfaSearch: program word offset of the 256-byte byte -> class map
+  uint32_t acc_mid_off;  // kDfaSearch: program: u32 pattern mask per mid-set id (256)
+  uint32_t acc_ncls;     // kDfaSearch: byte classes (row length of the dense table)
 };
-static_assert(sizeof(DfaDesc) == 96, "dfa desc is 24 words");
+static_assert(sizeof(DfaDesc) == 112, "dfa desc is 28 words");
+
+// Search automata (L7M_DIALECT_RE2_SEARCH regex fields, Go regexp
+// MatchString): a dense DFA of [\x00-\xff]*(p0|...|pk), k < 32, walked as
+//     e = T[state * ncls + cmap[b]];  state = e & 0xffffff;  acc |= mid[e >> 24]
+// where mid[] is the mask of the patterns whose match ends at this byte with
+// input left ('$' unsatisfied), and at the end acc |= es[state] (the patterns
+// matching at the end of the input).  acc -- the patterns matching some
+// substring -- is the walk's code: bit p = local pattern p.  start_base is the
+// start state, start_es8 its mid mask; nsets is 0, so candidate entry p is
+// the rules keyed on pattern p.
+constexpr uint32_t kDfaPacked = 0, kDfaSearch = 1;
+constexpr uint32_t kSearchMaxPats = 32, kSearchMaxMid = 256;
 
 // Candidate entry of one end code (16 words): the keyed rules' check records
 // (sorted by rule id) live in the check-record pool at [off, len records);
@@ -121,6 +137,7 @@ constexpr uint32_t kMaxLdsCounters = 8192;       // per-rule hit counters kept i
 constexpr uint32_t kHttpMinStage = 2048;         // smallest record stage per wave (bytes)
 constexpr uint32_t kHttpMaxStage = 8192;         // largest record stage per wave (bytes)
 constexpr uint32_t kMaxLdsCtmaskWords = 256;     // candidate-presence bitmask kept in LDS up to this
+constexpr uint32_t kHttpPrefetchSink = 256;      // LDS bytes the next tile's L2 prefetch writes (64 lanes x 4)
 
 struct FieldDesc {
   uint32_t dfa_first, ndfa;  // value DFAs of this field (contiguous)
@@ -183,14 +200,16 @@ struct HttpHeader {
   uint32_t cand_dfas_lo;   // bit d (n_dfas <= 64): value DFA d has candidate
   uint32_t cand_dfas_hi;   // entries for some end code (else verification skips it)
   uint32_t pres_fields_lo; // bit f: field f has a presence-keyed check-record list
-  uint32_t pres_fields_hi;  // header = 36 words
+  uint32_t pres_fields_hi;
+  uint32_t search;         // 1: some value DFA is a kDfaSearch automaton (RE2 dialect)
+  uint32_t pad[3];         // header = 40 words
 };
 // Header-name table (LDS image): exact lower-case header names of the rules
 // -> field id, open addressing on the program.h name hash; slot =
 // {hash (0 = empty), len, field, image word offset of the zero-padded name}.
 // Replaces the walk of the header-name DFA when it fits kMaxNameTabBytes.
 constexpr uint32_t kMaxNameTabBytes = 8192;
-static_assert(sizeof(HttpHeader) == 144, "header is 36 words");
+static_assert(sizeof(HttpHeader) == 160, "header is 40 words");
 
 // ---------------------------------------------------------------- Kafka --
 // Rule semantics follow pkg/kafka/policy.go:144-225 and

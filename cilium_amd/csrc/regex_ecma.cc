@@ -700,7 +700,25 @@ Ast literal_ast(const std::string& lit) {
   return a;
 }
 
-Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, Dfa* out) {
+void make_search_prefix(Ast* a) {
+  Node any;
+  any.kind = Node::Set;
+  any.set.set();
+  a->nodes.push_back(any);
+  Node star;
+  star.kind = Node::Rep;
+  star.kids = {static_cast<int>(a->nodes.size()) - 1};
+  star.min = 0;
+  star.max = -1;
+  a->nodes.push_back(star);
+  Node cat;
+  cat.kind = Node::Cat;
+  cat.kids = {static_cast<int>(a->nodes.size()) - 1, a->root};
+  a->nodes.push_back(cat);
+  a->root = static_cast<int>(a->nodes.size()) - 1;
+}
+
+Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, Dfa* out, bool with_mid) {
   Nfa nfa;
   std::vector<int> starts;
   try {
@@ -811,43 +829,44 @@ Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, 
   std::unordered_map<std::vector<uint32_t>, uint32_t, U32VecHash> set_ids;
   sets.push_back({});
   set_ids.emplace(std::vector<uint32_t>{}, 0);
-  std::vector<uint32_t> endset(n0, 0);
+  std::vector<uint32_t> endset(n0, 0), midset(n0, 0);
   std::vector<int> seed;
-  for (size_t d = 1; d < n0; ++d) {
-    bool is_start = !kern[d].empty() && kern[d][0] == -1;
-    seed.clear();
-    for (int s : kern[d])
-      if (s >= 0) seed.push_back(s);
-    clo.run(seed, is_start, true, &tmpk);
+  auto set_of = [&](bool is_start, bool eol) -> uint32_t {
+    clo.run(seed, is_start, eol, &tmpk);
     std::vector<uint32_t> pats;
     for (int s : tmpk)
       if (nfa.st[s].type == NState::MATCH) pats.push_back(static_cast<uint32_t>(nfa.st[s].pat));
     std::sort(pats.begin(), pats.end());
     pats.erase(std::unique(pats.begin(), pats.end()), pats.end());
     auto it = set_ids.find(pats);
-    uint32_t sid;
-    if (it == set_ids.end()) {
-      sid = static_cast<uint32_t>(sets.size());
-      set_ids.emplace(pats, sid);
-      sets.push_back(pats);
-    } else {
-      sid = it->second;
-    }
-    endset[d] = sid;
+    if (it != set_ids.end()) return it->second;
+    const uint32_t sid = static_cast<uint32_t>(sets.size());
+    set_ids.emplace(pats, sid);
+    sets.push_back(pats);
+    return sid;
+  };
+  for (size_t d = 1; d < n0; ++d) {
+    bool is_start = !kern[d].empty() && kern[d][0] == -1;
+    seed.clear();
+    for (int s : kern[d])
+      if (s >= 0) seed.push_back(s);
+    endset[d] = set_of(is_start, true);
+    if (with_mid) midset[d] = set_of(is_start, false);
   }
   kern.clear();
   kern.shrink_to_fit();
 
-  // Moore minimisation: initial partition by end set.
-  std::vector<uint32_t> blk(endset.begin(), endset.end());
-  size_t nblk = sets.size();
+  // Moore minimisation: initial partition by end set (and mid set).
+  std::vector<uint32_t> blk(n0);
+  size_t nblk = 0;
   {
     // dense renumber
-    std::unordered_map<uint32_t, uint32_t> rn;
-    for (auto& b : blk) {
-      auto it = rn.find(b);
-      if (it == rn.end()) it = rn.emplace(b, static_cast<uint32_t>(rn.size())).first;
-      b = it->second;
+    std::unordered_map<uint64_t, uint32_t> rn;
+    for (size_t s = 0; s < n0; ++s) {
+      const uint64_t key = static_cast<uint64_t>(midset[s]) << 32 | endset[s];
+      auto it = rn.find(key);
+      if (it == rn.end()) it = rn.emplace(key, static_cast<uint32_t>(rn.size())).first;
+      blk[s] = it->second;
     }
     nblk = rn.size();
   }
@@ -905,11 +924,13 @@ Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, 
   d.start = static_cast<int>(newid[blk[start_id]]);
   d.next.assign(nst * ncls, 0);
   d.endset.assign(nst, 0);
+  if (with_mid) d.midset.assign(nst, 0);
   for (size_t i = 0; i < nst; ++i) {
     size_t s = rep[order[i]];
     for (int c = 0; c < ncls; ++c)
       d.next[i * ncls + c] = static_cast<uint32_t>(newid[blk[next[s * ncls + c]]]);
     d.endset[i] = endset[s];
+    if (with_mid) d.midset[i] = midset[s];
   }
   d.sets = std::move(sets);
   *out = std::move(d);

@@ -62,6 +62,8 @@ struct Dfa {
   int start = 0;
   std::vector<uint32_t> next;   // nstates * ncls, next-state ids
   std::vector<uint32_t> endset; // nstates: id into sets (0 = empty set)
+  std::vector<uint32_t> midset; // nstates (build_dfa with_mid only): patterns matched here
+                                // when the input does NOT end here ('$' not satisfied)
   std::vector<std::vector<uint32_t>> sets;  // set id -> sorted pattern ids
 };
 
@@ -73,7 +75,16 @@ struct DfaLimits {
 // Determinise patterns[0..n) (pattern id = index) into one minimised DFA with
 // states numbered breadth-first from the start state.  Returns TooBig when a
 // limit is exceeded (caller splits the pattern set).
-Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, Dfa* out);
+Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, Dfa* out, bool with_mid = false);
+
+// Prefix a pattern with [\x00-\xff]* (a match may start anywhere): with
+// build_dfa's mid sets, the patterns matching a substring that ends at each
+// position of the input (regexp.MatchString = the union over positions).
+void make_search_prefix(Ast* a);
+
+// Cut a search pattern's trailing repetitions to their minimum (equivalent
+// under regexp.MatchString, regex_re2.cc).
+void simplify_search(Ast* a);
 
 }  // namespace re
 }  // namespace l7m

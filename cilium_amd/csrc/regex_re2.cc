@@ -465,6 +465,38 @@ Status parse_re2(const std::string& pat, Ast* out, std::string* err) {
 // MatchString is an unanchored search: the pattern may match any substring,
 // i.e. the whole subject matches [\x00-\xff]* p [\x00-\xff]* (p's own ^ / $
 // still assert the subject's ends).
+// Search semantics make a pattern's trailing repetitions redundant: a
+// subject contains p X{n,m} (or p X*) iff it contains p X{n} (p), so the
+// trailing elements of the top-level concatenation are cut down to their
+// minimum -- which keeps the per-pattern "inside the .* tail" states out of
+// a search automaton's product (config 2's `/api/w/.*` family).  Nothing
+// after them: a '$' keeps the pattern as it is.
+void simplify_search(Ast* a) {
+  std::vector<int> seq;
+  const Node& r = a->nodes[a->root];
+  if (r.kind == Node::Cat) seq = r.kids;
+  else seq.push_back(a->root);
+  while (!seq.empty()) {
+    const Node& n = a->nodes[seq.back()];
+    if (n.kind == Node::Rep && n.min == 0) {
+      seq.pop_back();
+      continue;
+    }
+    if (n.kind == Node::Rep && n.max != n.min) {
+      Node m = n;
+      m.max = m.min;
+      a->nodes.push_back(m);
+      seq.back() = static_cast<int>(a->nodes.size()) - 1;
+    }
+    break;
+  }
+  Node cat;
+  cat.kind = Node::Cat;
+  cat.kids = seq;
+  a->nodes.push_back(cat);
+  a->root = static_cast<int>(a->nodes.size()) - 1;
+}
+
 void make_search(Ast* a) {
   Node any;
   any.kind = Node::Set;

@@ -21,12 +21,15 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
               "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi "
-              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi").split()
+              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab "
-              "lds_skip skip_lim").split()
+              "lds_skip skip_lim kind acc_cmap_off acc_mid_off acc_ncls").split()
 SKIP_LOOP, SKIP_LIT = 1, 2  # program.h kSkipLoop / kSkipLit
+SKIP_MIN_REST = 64  # l7m_kernels.hip kSkipMinRest: bytes left for a skip row to be taken
 ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
+DFA_WORDS = 28  # sizeof(DfaDesc) / 4
+DFA_SEARCH = 1  # program.h kDfaSearch
 
 
 def name_hash(data: bytes) -> int:
@@ -51,17 +54,17 @@ class HttpProgram:
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
         h = self.h
         assert h["magic"] == 0x3448374C
-        assert len(HDR_FIELDS) == 36
+        assert len(HDR_FIELDS) == 37  # + 3 pad words (program.h HttpHeader, 40 words)
         io = h["lds_image_off"]
         self.img = self.w[io:io + h["lds_image_words"]]
         self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
         ndt = h["n_dfas"] + h["has_name_dfa"]
         self.dfas = []
         for k in range(ndt):
-            o = h["lds_dfas"] + 24 * k  # the kernel reads the LDS copy
+            o = h["lds_dfas"] + DFA_WORDS * k  # the kernel reads the LDS copy
             d = dict(zip(DFA_FIELDS, self.img[o:o + len(DFA_FIELDS)]))
-            g = h["off_dfas"] + 24 * k
-            assert self.w[g:g + 24] == self.img[o:o + 24]
+            g = h["off_dfas"] + DFA_WORDS * k
+            assert self.w[g:g + DFA_WORDS] == self.img[o:o + DFA_WORDS]
             self.dfas.append(d)
         self.fields = [tuple(self.img[h["lds_fields"] + 4 * f: h["lds_fields"] + 4 * f + 4])
                        for f in range(h["n_fields"])]
@@ -81,9 +84,23 @@ class HttpProgram:
                     return sl[2]
             at = (at + 1) & h["name_tab_mask"]
 
+    def walk_search(self, d, data: bytes):
+        """Search automaton (program.h kDfaSearch): mask of the patterns
+        matching some substring of data."""
+        cm = b"".join(int(x).to_bytes(4, "little") for x in self.w[d["acc_cmap_off"]:d["acc_cmap_off"] + 64])
+        ncls, T, mid = d["acc_ncls"], d["table_off"], d["acc_mid_off"]
+        st, acc = d["start_base"], d["start_es8"]
+        for b in data:
+            e = self.w[T + st * ncls + cm[b]]
+            st = e & 0xFFFFFF
+            acc |= self.w[mid + (e >> 24)]
+        return acc | self.w[d["es_off"] + st]
+
     def walk(self, k, data: bytes):
         """Packed double-array walk (cilium_amd/csrc/dfa_pack.h): end code."""
         d = self.dfas[k]
+        if d["kind"] == DFA_SEARCH:
+            return self.walk_search(d, data)
         lds = d["lds_table"] != KNONE
         base = d["start_base"]
         last = KNONE
@@ -138,7 +155,7 @@ class HttpProgram:
                         if st[0]:
                             step(c)
                     k += 8
-                    if st[0] and st[0] >= slim:
+                    if st[0] and st[0] >= slim and n - k >= SKIP_MIN_REST:
                         k = skip(k)
             while k < n and st[0]:
                 step(data[k])
@@ -172,6 +189,8 @@ class HttpProgram:
     def code_has(self, k, code, p):
         if code == 0:
             return False
+        if self.dfas[k]["kind"] == DFA_SEARCH:
+            return bool((code >> p) & 1)
         if code & LATCHED:
             return (code & ~LATCHED) == p
         d = self.dfas[k]
@@ -316,6 +335,11 @@ class HttpProgram:
         for k in range(h["n_dfas"]):
             code = codes[k]
             if not code:
+                continue
+            if self.dfas[k]["kind"] == DFA_SEARCH:  # candidates of every matched pattern
+                for p in range(32):
+                    if (code >> p) & 1:
+                        best = scan(self.ct(k, p), best)
                 continue
             idx = self.dfas[k]["nsets"] + (code & ~LATCHED) if code & LATCHED else code
             best = scan(self.ct(k, idx), best)

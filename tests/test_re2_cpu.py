@@ -12,6 +12,7 @@ import pytest
 from cilium_amd import l7match as L
 from oracle import HttpOracle, regex_search
 from program_interp import HttpProgram
+from cilium_amd import workloads as W
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "re2_search.json")
 RE2 = L.DIALECT_RE2_SEARCH
@@ -87,3 +88,32 @@ def test_multi_rule_first_match_vs_oracle():
     exp = HttpOracle(rules, dialect=RE2).eval(arena, offs)
     bad = np.nonzero(got != exp)[0]
     assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+def test_config2_1k_rules_compile_as_search_automata():
+    """BASELINE config 2's 1000 rules compile under the RE2 dialect (search
+    automata, program.h kDfaSearch: trailing repetitions cut, <= 32 patterns
+    per automaton) and the program interpreter agrees with the oracle."""
+    rules = W.rules(2)
+    rs = L.RuleSet.compile_http(rules, dialect=RE2)
+    prog = HttpProgram(rs.program())
+    assert prog.h["search"] == 1
+    kinds = [d["kind"] for d in prog.dfas[:prog.h["n_dfas"]]]
+    assert kinds.count(1) >= 1000 // 32
+    arena, offs = W.requests(2, 0, 1500)
+    got = prog.eval(arena, offs)
+    exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+def test_search_trailing_repetition_cut_is_exact():
+    """simplify_search: p X* / p X{n,m} at the end of a pattern match exactly
+    where p / p X{n} do under search semantics; '$' after them keeps them."""
+    cases = [("/a/.*", ["/a/", "x/a/", "/a", "/a/\nz"]), ("ab+", ["a", "ab", "xabbb"]),
+             ("ab{2,4}", ["ab", "abb", "zabbbbbb"]), ("ab*$", ["a", "ab", "abx", "xabb"]),
+             ("x*", ["", "y"]), ("(ab|cd)+", ["ab", "cdab", "ac"])]
+    for pattern, subjects in cases:
+        subs = [s.encode() for s in subjects]
+        got = _interp_paths(pattern, subs)
+        assert [int(v) == 0 for v in got] == [bool(regex_search(pattern, s)) for s in subs], pattern

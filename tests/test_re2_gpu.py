@@ -1,6 +1,7 @@
 """L7M_DIALECT_RE2_SEARCH on the GPU through the C ABI: golden vectors
 (tests/golden/re2_search.json) and multi-rule batches against the oracle
-(std::regex_search), bit-exact verdicts."""
+(std::regex_search), bit-exact verdicts -- including BASELINE config 2's
+1k-rule set compiled as search automata (program.h kDfaSearch)."""
 import json
 import os
 
@@ -9,6 +10,7 @@ import pytest
 
 from cilium_amd import l7match as L
 from oracle import HttpOracle
+from cilium_amd import workloads as W
 
 pytestmark = pytest.mark.gpu
 RE2 = L.DIALECT_RE2_SEARCH
@@ -49,3 +51,38 @@ def test_multi_rule_batches_vs_oracle(gpu):
         exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
         bad = np.nonzero(got != exp)[0]
         assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+
+
+def test_config2_1k_rules_search_vs_oracle(gpu):
+    """BASELINE config 2's 1000 rules under Go MatchString semantics: 32 path
+    search automata + method / host automata, 20k requests, bit-exact."""
+    rules = W.rules(2)
+    rs = L.RuleSet.compile_http(rules, dialect=RE2)
+    arena, offs = W.requests(2, 5_000_000, 20_000)
+    got = rs.eval(arena, offs)
+    exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+    assert (exp >= 0).mean() > 0.3  # the search set decides most requests by a rule
+
+
+def test_golden_vectors_at_1k_rules(gpu):
+    """The golden search vectors' patterns ahead of the 1000 config-2 rules:
+    the verdict of a golden subject is its first matching rule (oracle), and a
+    golden "match" / "no match" fixes whether the pattern's own rule can be it."""
+    cases = golden()["search"]
+    pats = sorted({c["pattern"] for c in cases})
+    idx = {p: i for i, p in enumerate(pats)}
+    rules = [L.PortRuleHTTP(Path=p) for p in pats] + W.rules(2)
+    assert len(rules) >= 1000
+    rs = L.RuleSet.compile_http(rules, dialect=RE2)
+    arena, offs = L.pack_http([L.HTTPRequest("GET", c["subject"].encode("latin-1"), "h") for c in cases])
+    got = rs.eval(arena, offs)
+    exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
+    assert np.array_equal(got, exp)
+    for c, v in zip(cases, got.tolist()):
+        r = idx[c["pattern"]]
+        if c["match"]:
+            assert 0 <= v <= r, c
+        else:
+            assert v != r, c
