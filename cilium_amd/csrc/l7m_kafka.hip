@@ -118,7 +118,21 @@ struct RdL {
   __device__ static __forceinline__ uint64_t be(Rd& d, uint32_t n) {
     const bool ok = !d.err && d.len - d.pos >= n;
     uint64_t v = 0;
+#ifdef L7M_KPERM
+    // big-endian field from the two aligned stage words holding it: one
+    // v_perm picks its bytes (records start 4-byte aligned in the stage)
+    if (n == 2 || n == 4) {
+      const uint32_t q = d.pos;
+      const uint32_t* a = reinterpret_cast<const uint32_t*>(d.p + (q & ~3u));
+      const uint32_t w0 = a[0], w1 = a[1], sh = q & 3u;
+      const uint32_t sel = n == 4 ? 0x00010203u + sh * 0x01010101u : 0x0c0c0001u + sh * 0x00000101u;
+      v = __builtin_amdgcn_perm(w1, w0, sel);
+    } else {
+      for (uint32_t i = 0; i < n; ++i) v = (v << 8) | d.p[d.pos + i];
+    }
+#else
     for (uint32_t i = 0; i < n; ++i) v = (v << 8) | d.p[d.pos + i];
+#endif
     d.err = !ok;
     d.pos = ok ? d.pos + n : d.len;
     return ok ? v : 0;
@@ -546,19 +560,39 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       // names against the slots' inline prefixes (same cache line).
       uint32_t hs[kTopicQ];
       u32x4 hd[kTopicQ];
+#ifdef L7M_KSLOT32
+      u32x4 hp[kTopicQ];  // the slots' inline name prefixes, fetched with the heads
+#endif
 #pragma unroll
       for (uint32_t r = 0; r < kTopicQ; ++r) {
         hs[r] = 0;
         hd[r] = u32x4{0u, 0u, 0u, 0u};
+#ifdef L7M_KSLOT32
+        hp[r] = u32x4{0u, 0u, 0u, 0u};
+#endif
         if (r < nq && maxf != kNone) {
           const uint32_t toff = tq[64 * r];
           const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
           if (tlen && tlen <= kMaxTopicLen && v.n_slots) {
             hs[r] = load_name<kLds>(rec + toff, tlen).hash;
             hd[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[0];
+#ifdef L7M_KSLOT32
+            hp[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[1];
+#endif
           }
         }
       }
+#ifdef L7M_KPF2
+      // the home slots' inline name prefixes (same lines as the heads, L1
+      // hits by now), all requested before the first compare
+      u32x4 hp[kTopicQ];
+#pragma unroll
+      for (uint32_t r = 0; r < kTopicQ; ++r) {
+        hp[r] = u32x4{0u, 0u, 0u, 0u};
+        if (r < nq && maxf != kNone && hs[r] && hd[r].x != 0)
+          hp[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[1];
+      }
+#endif
 #pragma unroll
       for (uint32_t r = 0; r < kTopicQ; ++r) {
         if (r < nq && maxf != kNone) {
@@ -572,7 +606,11 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
             sl.meta = hd[r].y;
             sl.r0 = hd[r].z;
             sl.r0_client = hd[r].w;
+#if defined(L7M_KSLOT32) || defined(L7M_KPF2)
+            const u32x4 pf = hp[r];
+#else
             const u32x4 pf = reinterpret_cast<const u32x4*>(v.slots + at)[1];
+#endif
             sl.pfx[0] = pf.x;
             sl.pfx[1] = pf.y;
             sl.pfx[2] = pf.z;
@@ -614,6 +652,11 @@ constexpr uint32_t kKMaxLdsCounters = 16384;
 constexpr uint32_t kSpanLds = (4 * kKafkaKinds + 3) & ~3u;  // words
 constexpr uint32_t kKindOkLds = (2 * kKafkaKinds + 3) & ~3u;  // words
 constexpr uint32_t kMaxCliLdsBytes = 8192;  // client table copied to LDS up to this size
+#ifdef L7M_KDMA
+constexpr uint32_t kKPrefetchSink = 256;  // LDS bytes of the next tile's L2 prefetch (64 lanes x 4)
+#else
+constexpr uint32_t kKPrefetchSink = 0;
+#endif
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
   const uint32_t lo = __shfl(static_cast<uint32_t>(x), src);
@@ -660,7 +703,12 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   const uint32_t cli_words = kCliLds ? h.n_clients * (sizeof(KafkaClientSlot) / 4) : 0u;
   uint32_t* ctr = cli + cli_words;
   uint16_t* tq = reinterpret_cast<uint16_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
+#ifdef L7M_KDMA
+  uint8_t* pfz = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ);  // L2-prefetch sink (never read)
+  uint8_t* stg = pfz + kKPrefetchSink + wv * (stage + 16u);
+#else
   uint8_t* stg = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ) + wv * (stage + 16u);
+#endif
   tq += wv * 64 * kTopicQ + lane;
   if (kCliLds)
     for (uint32_t i = tid; i < cli_words; i += kKBlock) cli[i] = prog[h.off_clients + i];
@@ -721,6 +769,26 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     t.take = t.k ? t.k : 1u;
     return t;
   };
+#ifdef L7M_KDMA
+  // LDS-DMA staging (global_load_lds_dwordx4, non-temporal), issued after the
+  // tile's decode and lookups (the stage's only readers); the next tile's
+  // window is pulled into L2 at the top of the iteration (one 4-byte LDS-DMA
+  // per 128-byte line into a sink), so the copy waits for L2, not HBM, and
+  // no registers hold in-flight bytes through the decode.
+  auto issue_bytes = [&](const Tile& t) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's stage reads are done
+#pragma unroll
+    for (uint32_t it = 0; it < kKCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < t.bytes)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(stg + it * 1024u)),
+                                         16, 0, 2);
+    }
+  };
+#else
   u32x4 buf[kKCopyIters];
   auto issue_bytes = [&](const Tile& t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
@@ -730,12 +798,23 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
       if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
     }
   };
+#endif
   uint64_t o1, n1, o2, n2;
   load_offs(n * gw / nw, &o1, &n1);
   Tile t = plan(n * gw / nw, o1, n1);
   issue_bytes(t);
   load_offs(t.cur + t.take, &o2, &n2);
   while (t.cur < end) {
+#ifdef L7M_KDMA
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
+    wave_sync();
+    const Tile t2 = plan(t.cur + t.take, o2, n2);
+    if (lane * 128u < t2.bytes)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(arena + t2.base + lane * 128u),
+                                       reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                           reinterpret_cast<uintptr_t>(pfz)),
+                                       4, 0, 0);
+#else
 #pragma unroll
     for (uint32_t it = 0; it < kKCopyIters; ++it) {
       const uint32_t q = it * 64u + lane;
@@ -745,6 +824,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     const Tile t2 = plan(t.cur + t.take, o2, n2);
     issue_bytes(t2);
     load_offs(t2.cur + t2.take, &o2, &n2);
+#endif
 
     const uint64_t o = t.o, onext = t.onext;
     int32_t verdict = 0;
@@ -793,6 +873,10 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
       }
       verdicts[t.cur + lane] = verdict;
     }
+#ifdef L7M_KDMA
+    issue_bytes(t2);  // the stage's readers are done
+    load_offs(t2.cur + t2.take, &o2, &n2);
+#endif
 #ifdef L7M_PROF
     prof[4] += __builtin_amdgcn_s_memtime() - te0;
 #endif
@@ -852,7 +936,7 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const bool cli_lds = cli_words && cli_words * 4 <= kMaxCliLdsBytes;
   const size_t fixed = 4u * (256u + kSpanLds + kKindOkLds + (cli_lds ? cli_words : 0u) +
                              (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
-                       2u * kKWaves * 64 * kTopicQ;
+                       2u * kKWaves * 64 * kTopicQ + kKPrefetchSink;
   size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
   stage &= ~size_t(15);
   if (stage > kKMaxStage) stage = kKMaxStage;
