@@ -214,7 +214,7 @@ struct LdsChain {
     lim = dd.lds_table + dd.region;
     sel = ((dd.lds_table + dd.start_base) << kLdsRowShift) | (dd.start_es8 << 8);
     slast = kNone;
-#ifndef L7M_NO_SKIP
+#ifdef L7M_SKIP
     slim = dd.lds_skip != kNone ? dd.lds_table + (dd.skip_lim & 0xffffu) : ~0u;
     sk = dd.lds_skip;
     lw = dd.lds_skip - (dd.skip_lim >> 16);
@@ -296,7 +296,7 @@ struct LdsChain {
       L7M_STEP(b7)
       k += 8;
       if (dead_now()) return;
-#ifndef L7M_NO_SKIP
+#ifdef L7M_SKIP
       // staged records (HBM-direct ones walk every byte: less code), and only
       // with a long rest: a lane in the skip handler runs its own loop while
       // the wave's other lanes wait, which costs more than walking a short
@@ -397,6 +397,18 @@ struct Codes<8> {
     const uint32_t lo = d & 2 ? b : a, hi = d & 2 ? f : e;
     return d & 4 ? hi : lo;
   }
+  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) {  // d wave-uniform
+    switch (d) {
+      case 0: r0 = v; break;
+      case 1: r1 = v; break;
+      case 2: r2 = v; break;
+      case 3: r3 = v; break;
+      case 4: r4 = v; break;
+      case 5: r5 = v; break;
+      case 6: r6 = v; break;
+      default: r7 = v; break;
+    }
+  }
 };
 template <>
 struct Codes<4> {  // programs with <= 4 value DFAs: four registers
@@ -412,6 +424,14 @@ struct Codes<4> {  // programs with <= 4 value DFAs: four registers
     const uint32_t a = d & 1 ? r1 : r0, b = d & 1 ? r3 : r2;
     return d & 2 ? b : a;
   }
+  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) {  // d wave-uniform
+    switch (d) {
+      case 0: r0 = v; break;
+      case 1: r1 = v; break;
+      case 2: r2 = v; break;
+      default: r3 = v; break;
+    }
+  }
 };
 template <>
 struct Codes<0> {
@@ -420,6 +440,7 @@ struct Codes<0> {
     for (uint32_t d = 0; d < n; ++d) p[d * kBlock] = 0;
   }
   __device__ __forceinline__ void set(uint32_t d, uint32_t v) { p[d * kBlock] = v; }
+  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) { p[d * kBlock] = v; }
   __device__ __forceinline__ uint32_t get(uint32_t d) const { return p[d * kBlock]; }
 };
 
@@ -437,6 +458,7 @@ struct Codes<-1> {
   __device__ __forceinline__ void set(uint32_t d, uint32_t v) {
     __hip_atomic_store(p + d * stride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) { set(d, v); }
   __device__ __forceinline__ uint32_t get(uint32_t d) const {
     uint32_t v = __hip_atomic_load(p + d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" : "+v"(v));
@@ -449,6 +471,8 @@ struct Ctx {
   const uint32_t* img;         // LDS image
   const DfaDesc* dds;          // LDS
   const FieldDesc* fields;     // LDS
+  const DfaDesc* __restrict__ gdds;       // program copies (uniform reads: scalar loads)
+  const FieldDesc* __restrict__ gfields;
   const uint32_t* name_field;  // LDS
   const Span* sets;            // HBM
   const uint32_t* pool;        // HBM
@@ -473,6 +497,14 @@ __device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd,
     acc |= gld(mid + (e >> 24));
   }
   return acc | gld(c.prog + dd.es_off + st);
+}
+
+template <bool kLit, bool kSearch, class Src>
+__device__ __forceinline__ uint32_t walk_desc(const Ctx& c, const DfaDesc& dd, const Src& src, uint32_t pos,
+                                              uint32_t len) {
+  if (kSearch && dd.kind == kDfaSearch) return walk_search(c, dd, src, pos, len);
+  if (dd.lds_table != kNone) return walk_lds(c.img, c.prog, dd, src, pos, len);
+  return walk_hbm<kLit>(c.img, c.prog, dd, src, pos, len);
 }
 
 template <bool kLit, bool kSearch, class Src>
@@ -703,6 +735,30 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         ++hj;
       }
     }
+#ifdef L7M_UNIFORM
+    // The lanes' fields, one at a time (a waterfall; the pseudo-header jobs
+    // take one round): inside a round the field and its DFAs are
+    // wave-uniform, so their descriptors are scalar loads of the program's
+    // copies (SGPRs, no per-lane descriptor arithmetic) and the end code goes
+    // to its register by a uniform branch.
+    if (f != kNone) present |= 1ull << f;
+    bool todo = f != kNone;
+    for (;;) {
+      const uint64_t m = __ballot(todo);
+      if (!m) break;
+      const uint32_t fu = __builtin_amdgcn_readlane(f, static_cast<uint32_t>(__builtin_ctzll(m)));
+      if (todo && f == fu) {
+        todo = false;
+        const FieldDesc& fd = c.gfields[fu];
+        for (uint32_t k = 0; k < fd.ndfa; ++k) {
+          const uint32_t d = fd.dfa_first + k;
+          const uint32_t code = walk_desc<kLit, (kReg < 0)>(c, c.gdds[d], src, p, len);
+          codes.set_u(d, code);
+          touch(d, code);
+        }
+      }
+    }
+#else
     if (f != kNone) {
       present |= 1ull << f;
       const FieldDesc& fd = c.fields[f];
@@ -713,6 +769,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         touch(d, code);
       }
     }
+#endif
   }
 
   HPROF(5);
@@ -743,6 +800,10 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
                                                const u32x4 (&pe)[3]) {
   const Codes<kReg>& codes = o.codes;
   const uint64_t present = o.present;
+#ifndef L7M_EPF
+  (void)pe;
+  asm volatile("" ::"v"(o.pf_t));  // the touch completes here, not at its first use
+#endif
   const uint32_t ex = o.ex, e0 = o.e0, remote = o.remote;
   const bool h0 = o.h0;
   // a rule may decide only if it belongs to ex, or to e0 when e0 has HTTP rules
@@ -851,9 +912,11 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
     if (!((mw >> (idx & 31u)) & 1u)) continue;  // no candidates
     if (dd.lds_ct != kNone) {
       check_inline(c.img + dd.lds_ct + 16u * idx);
+#ifdef L7M_EPF
     } else if (d == o.pf_d) {
       check_entry(pe[0], pe[1], pe[2]);
-    } else {  // a further HBM candidate entry (not prefetched)
+#endif
+    } else {  // an HBM candidate entry (L7M_EPF: one that was not prefetched)
       typedef __attribute__((address_space(1))) const u32x4* gq;
       const gq q = (gq)(c.prog + dd.ct_off + 16u * idx);
       u32x4 q0 = q[0], q1 = q[1], q2 = q[2];
@@ -922,6 +985,8 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
   c.img = img;
   c.dds = reinterpret_cast<const DfaDesc*>(img + h.lds_dfas);
   c.fields = reinterpret_cast<const FieldDesc*>(img + h.lds_fields);
+  c.gdds = reinterpret_cast<const DfaDesc*>(prog + h.off_dfas);
+  c.gfields = reinterpret_cast<const FieldDesc*>(prog + h.off_fields);
   c.name_field = img + h.lds_name_field;
   c.sets = reinterpret_cast<const Span*>(prog + h.off_sets);
   c.pool = prog + h.off_pool;
@@ -996,51 +1061,57 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
     t.take = t.k ? t.k : 1u;
     return t;
   };
-#ifdef L7M_REGSTAGE
+  // Staging.  Register staging (the default): the next tile's bytes are
+  // loaded into VGPRs after the walks and written to the stage at the top of
+  // the next iteration.  LDS-DMA staging (global_load_lds_dwordx4,
+  // non-temporal; the literal-table instantiation, or L7M_LDSDMA): the bytes
+  // go HBM -> the wave's stage with no VGPR destination and no ds_write pass
+  // (lane l of piece `it` lands at stage + it * 1 KiB + 16 l, the coalesced
+  // copy's own layout), issued after the walks, the stage's only readers.
+  // Measured: registers are 2 % faster on config 2; LDS-DMA removes the
+  // literal instantiation's VGPR spills (config 5 1.277 -> 1.266 ms).
+#ifdef L7M_LDSDMA
+  constexpr bool kDma = true;
+#else
+  constexpr bool kDma = kLit;
+#endif
   u32x4 buf[kCopyIters];
   auto issue_bytes = [&](const Tile& t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
+    if constexpr (kDma) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's stage reads are done
 #pragma unroll
-    for (uint32_t it = 0; it < kCopyIters; ++it) {
-      const uint32_t q = it * 64u + lane;
-      if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
+      for (uint32_t it = 0; it < kCopyIters; ++it) {
+        const uint32_t q = it * 64u + lane;
+        if (q * 16u < t.bytes)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
+                                           reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                               reinterpret_cast<uintptr_t>(stg + it * 1024u)),
+                                           16, 0, 2);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t it = 0; it < kCopyIters; ++it) {
+        const uint32_t q = it * 64u + lane;
+        if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
+      }
     }
   };
-#else
-  // LDS-DMA staging (global_load_lds_dwordx4, non-temporal): the tile's bytes
-  // go HBM -> the wave's stage with no VGPR destination and no ds_write pass;
-  // lane l of piece `it` lands at stage + it * 1 KiB + 16 l (the coalesced
-  // copy's own layout).  Issued after the walks, the only readers of the
-  // stage; the next loop iteration waits for it before reading.
-  auto issue_bytes = [&](const Tile& t) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's stage reads are done
-#pragma unroll
-    for (uint32_t it = 0; it < kCopyIters; ++it) {
-      const uint32_t q = it * 64u + lane;
-      if (q * 16u < t.bytes)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
-                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                             reinterpret_cast<uintptr_t>(stg + it * 1024u)),
-                                         16, 0, 2);
-    }
-  };
-#endif
   uint64_t o1, n1, o2, n2;
   load_offs(n * gw / nw, &o1, &n1);
   Tile t = plan(n * gw / nw, o1, n1);
   issue_bytes(t);
   load_offs(t.cur + t.take, &o2, &n2);
   while (t.cur < end) {
-#ifdef L7M_REGSTAGE
+    if constexpr (kDma) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
+    } else {
 #pragma unroll
-    for (uint32_t it = 0; it < kCopyIters; ++it) {
-      const uint32_t q = it * 64u + lane;
-      if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+      for (uint32_t it = 0; it < kCopyIters; ++it) {
+        const uint32_t q = it * 64u + lane;
+        if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+      }
     }
-#else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
-#endif
     wave_sync();
     QTN(0);
 #ifdef L7M_L2PF
@@ -1086,12 +1157,13 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
         v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
       }
     }
-    // The candidate entry the walks touched is loaded (an L1/L2 hit by now)
-    // and waited for BEFORE the next tile's bytes are requested: vmcnt is
-    // in-order, so verification reading it later would wait for the whole
-    // next tile from HBM.
     QTN(1);
     u32x4 pe[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#ifdef L7M_EPF
+    // (experiment, measured 1 % slower on config 2) the touched candidate
+    // entry is loaded and waited for BEFORE the next tile's bytes are
+    // requested: vmcnt is in-order, so verification reading it later waits
+    // for those bytes too
     if (lane < take && v == kNeedVerify && wo.pf_ent != kNone) {
       asm volatile("" ::"v"(wo.pf_t));  // the touch completes here, not at its first use
       const u32x4* e = reinterpret_cast<const u32x4*>(c.prog + wo.pf_ent);
@@ -1100,6 +1172,7 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
       pe[2] = e[2];
     }
     asm volatile("" : "+v"(pe[0]), "+v"(pe[1]), "+v"(pe[2]));  // landed here
+#endif
     QTN(2);
     // The next tile's bytes are requested only now, after the walks: they
     // land during verification without holding kCopyIters x 4 registers
