@@ -860,14 +860,61 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
       if (rid >= best) return;
       const uint32_t ma[4] = {q1.x, q1.z, q2.x, q2.z}, mp[4] = {q1.y, q1.w, q2.y, q2.w};
       bool ok = eligible(hd) && (!(hd & kCrRemote) || remote_ok(rid));
+#ifndef L7M_VSERIAL
+      if constexpr (kReg < 0)
+#endif
+      {  // search programs (mask codes): one matcher after the other
 #pragma unroll
-      for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {
-        if (q < nm && ok) {
-          const uint32_t a = ma[q];
-          if (!((present >> (a & 0xffu)) & 1ull)) ok = false;
-          else if (!((a >> 8) & 1u)) ok = code_has<(kReg < 0)>(c, a >> 9, codes.get(a >> 9), mp[q]);
+        for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {
+          if (q < nm && ok) {
+            const uint32_t a = ma[q];
+            if (!((present >> (a & 0xffu)) & 1ull)) ok = false;
+            else if (!((a >> 8) & 1u)) ok = code_has<(kReg < 0)>(c, a >> 9, codes.get(a >> 9), mp[q]);
+          }
         }
       }
+#ifndef L7M_VSERIAL
+      else
+      // The inline matchers in two rounds of independent LDS reads (each
+      // DFA's mask table, then the set's mask word) instead of one dependent
+      // chain per matcher; set codes whose masks are not in LDS (or search
+      // automata) take the general code_has.
+      {
+        uint32_t cq[4], mo[4], w[4];
+        bool need[4], set[4];
+#pragma unroll
+        for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {  // round 1: the DFAs' mask tables
+          const uint32_t a = ma[q];
+          cq[q] = q < nm ? codes.get(a >> 9) : 0u;
+          need[q] = q < nm && !((a >> 8) & 1u);  // a code matcher (else presence only)
+          set[q] = need[q] && cq[q] && !(cq[q] & kLatchedBit);
+          mo[q] = lld(reinterpret_cast<const uint32_t*>(c.dds + (a >> 9)) + offsetof(DfaDesc, lds_mask) / 4);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {  // round 2: the sets' mask words
+          const bool rd = set[q] && mo[q] != kNone;
+          w[q] = lld(c.img + (rd ? mo[q] + 2u * cq[q] + (mp[q] >> 5) : 0u));
+        }
+        bool slow = false;
+#pragma unroll
+        for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {
+          const uint32_t a = ma[q], p = mp[q];
+          const bool pres = q >= nm || ((present >> (a & 0xffu)) & 1ull);
+          const bool lat = (cq[q] & kLatchedBit) != 0;
+          const bool hit = !need[q] || (cq[q] != 0 && (lat ? (cq[q] & ~kLatchedBit) == p
+                                                           : (mo[q] == kNone || ((w[q] >> (p & 31u)) & 1u))));
+          slow |= set[q] && mo[q] == kNone;
+          ok = ok && pres && hit;
+        }
+        if (slow && ok) {  // rare: sets whose masks are in the program pool
+#pragma unroll
+          for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {
+            if (q < nm && ok && need[q] && cq[q] && !(cq[q] & kLatchedBit) && mo[q] == kNone)
+              ok = code_has<(kReg < 0)>(c, ma[q] >> 9, cq[q], mp[q]);
+          }
+        }
+      }
+#endif
       if (ok) best = rid;
     } else {
       scan(Span{q0.y, len});
@@ -934,6 +981,14 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
   if (best != kNone) return static_cast<int32_t>(best);
   // the exact-port entry matched nothing; a port-0 entry without HTTP rules allows
   return h0 ? L7M_VERDICT_DENY : L7M_VERDICT_ALLOW_NO_L7;
+}
+
+// A wave-uniform lane's 64-bit value: v_readlane (no LDS round trip, unlike
+// the ds_bpermute of __shfl); `src` must be wave-uniform.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t src) {
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), src);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), src);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
@@ -1050,14 +1105,14 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
       return t;
     }
     const uint64_t m = end - cur < 64 ? end - cur : 64;
-    const uint64_t o0 = shfl64(o, 0);
+    const uint64_t o0 = readlane64(o, 0);
     t.base = o0 & ~15ull;
     // Leading run of records that lie, in order, inside a window <= stage.
     const bool ok = lane < m && (o & 3) == 0 && o >= o0 && onext >= o && onext <= arena_bytes &&
                     onext - t.base <= stage;
     const uint64_t okm = __ballot(ok);
     t.k = okm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~okm));
-    t.bytes = t.k ? static_cast<uint32_t>(shfl64(onext, t.k - 1) - t.base) : 0u;
+    t.bytes = t.k ? static_cast<uint32_t>(readlane64(onext, t.k - 1) - t.base) : 0u;
     t.take = t.k ? t.k : 1u;
     return t;
   };
@@ -1195,7 +1250,11 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
       if (lane < take && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY)
         slot = v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u);
       if (kHits == kLdsHits) {
-        if (slot != kNone) atomicAdd(ctr + slot, 1u);
+        // denies / errors are common: one add per wave for them
+        const uint64_t dm = __ballot(slot == 0u), em = __ballot(slot == 1u);
+        if (lane == 0 && dm) atomicAdd(ctr, static_cast<uint32_t>(__popcll(dm)));
+        if (lane == 0 && em) atomicAdd(ctr + 1, static_cast<uint32_t>(__popcll(em)));
+        if (slot != kNone && slot >= 2u) atomicAdd(ctr + slot, 1u);
       } else {
         count_slot(hits, slot, slot != kNone);
       }
