@@ -683,9 +683,12 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     }
     // skip descriptors (dfa_pack.h): the literal pool, then one word per
     // skip-row base; only with the table in LDS and when they fit too
+    // (only for kernels built with L7M_SKIP: the descriptors cost image space,
+    // i.e. record stage, and the kernel's skip handler measured slower on
+    // config 2)
     const uint64_t pool_words = ((d.skip_lits.size() + 3) / 4 + 3) & ~uint64_t(3);  // img_take granules
-    if (dd[k].lds_table != kNone && d.skip_lim && d.skip_lim < (1u << 16) && pool_words < (1u << 15) &&
-        img + pool_words + d.skip.size() + 8 <= budget) {
+    if (kSkipRowsInKernel && dd[k].lds_table != kNone && d.skip_lim && d.skip_lim < (1u << 16) &&
+        pool_words < (1u << 15) && img + pool_words + d.skip.size() + 8 <= budget) {
       img_take(pool_words);
       dd[k].lds_skip = img_take(d.skip.size());
       dd[k].skip_lim = d.skip_lim | static_cast<uint32_t>(pool_words) << 16;
