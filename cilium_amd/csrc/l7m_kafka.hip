@@ -800,10 +800,13 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   u32x4 buf[kKCopyIters];
   auto issue_bytes = [&](const Tile& t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
+    const uint32_t qlast = t.bytes ? (t.bytes - 1u) / 16u : 0u;
 #pragma unroll
     for (uint32_t it = 0; it < kKCopyIters; ++it) {
       const uint32_t q = it * 64u + lane;
-      if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
+      // unconditional (no exec-mask branch per piece): lanes past the window
+      // load its last piece again (same line, no extra traffic)
+      if (t.bytes) buf[it] = __builtin_nontemporal_load(src + (q < qlast ? q : qlast));
     }
   };
 #endif
@@ -826,7 +829,12 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
 #pragma unroll
     for (uint32_t it = 0; it < kKCopyIters; ++it) {
       const uint32_t q = it * 64u + lane;
-      if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+      // whole pieces inside the stage: a uniform test, no exec-mask branch
+      if (it * 1024u + 1024u <= stage) {
+        if (t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+      } else if (q * 16u < t.bytes) {
+        reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+      }
     }
     wave_sync();
     const Tile t2 = plan(t.cur + t.take, o2, n2);

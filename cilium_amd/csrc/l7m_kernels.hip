@@ -1145,10 +1145,13 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
                                            16, 0, 2);
       }
     } else {
+      const uint32_t qlast = t.bytes ? (t.bytes - 1u) / 16u : 0u;
 #pragma unroll
       for (uint32_t it = 0; it < kCopyIters; ++it) {
         const uint32_t q = it * 64u + lane;
-        if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
+        // unconditional (no exec-mask branch per piece): lanes past the window
+        // load its last piece again (same line, no extra traffic)
+        if (t.bytes) buf[it] = __builtin_nontemporal_load(src + (q < qlast ? q : qlast));
       }
     }
   };
@@ -1164,7 +1167,12 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
 #pragma unroll
       for (uint32_t it = 0; it < kCopyIters; ++it) {
         const uint32_t q = it * 64u + lane;
-        if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+        // whole pieces inside the stage: a uniform test, no exec-mask branch
+        if (it * 1024u + 1024u <= stage) {
+          if (t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+        } else if (q * 16u < t.bytes) {
+          reinterpret_cast<u32x4*>(stg)[q] = buf[it];
+        }
       }
     }
     wave_sync();
