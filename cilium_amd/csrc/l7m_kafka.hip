@@ -658,14 +658,6 @@ constexpr uint32_t kKPrefetchSink = 256;  // LDS bytes of the next tile's L2 pre
 constexpr uint32_t kKPrefetchSink = 0;
 #endif
 
-// A wave-uniform lane's 64-bit value: v_readlane (no LDS round trip, unlike
-// the ds_bpermute of __shfl); `src` must be wave-uniform.
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t src) {
-  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), src);
-  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), src);
-  return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
   const uint32_t lo = __shfl(static_cast<uint32_t>(x), src);
   const uint32_t hi = __shfl(static_cast<uint32_t>(x >> 32), src);
@@ -767,13 +759,13 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
       return t;
     }
     const uint64_t m = end - cur < 64 ? end - cur : 64;
-    const uint64_t o0 = readlane64(o, 0);
+    const uint64_t o0 = shfl64(o, 0);
     t.base = o0 & ~15ull;
     const bool ok = lane < m && (o & 3) == 0 && o >= o0 && onext >= o && onext <= arena_bytes &&
                     onext - t.base <= stage;
     const uint64_t okm = __ballot(ok);
     t.k = okm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~okm));
-    t.bytes = t.k ? static_cast<uint32_t>(readlane64(onext, t.k - 1) - t.base) : 0u;
+    t.bytes = t.k ? static_cast<uint32_t>(shfl64(onext, t.k - 1) - t.base) : 0u;
     t.take = t.k ? t.k : 1u;
     return t;
   };
@@ -800,13 +792,10 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   u32x4 buf[kKCopyIters];
   auto issue_bytes = [&](const Tile& t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
-    const uint32_t qlast = t.bytes ? (t.bytes - 1u) / 16u : 0u;
 #pragma unroll
     for (uint32_t it = 0; it < kKCopyIters; ++it) {
       const uint32_t q = it * 64u + lane;
-      // unconditional (no exec-mask branch per piece): lanes past the window
-      // load its last piece again (same line, no extra traffic)
-      if (t.bytes) buf[it] = __builtin_nontemporal_load(src + (q < qlast ? q : qlast));
+      if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
     }
   };
 #endif
@@ -829,12 +818,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
 #pragma unroll
     for (uint32_t it = 0; it < kKCopyIters; ++it) {
       const uint32_t q = it * 64u + lane;
-      // whole pieces inside the stage: a uniform test, no exec-mask branch
-      if (it * 1024u + 1024u <= stage) {
-        if (t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
-      } else if (q * 16u < t.bytes) {
-        reinterpret_cast<u32x4*>(stg)[q] = buf[it];
-      }
+      if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
     }
     wave_sync();
     const Tile t2 = plan(t.cur + t.take, o2, n2);
@@ -900,11 +884,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
       uint32_t slot = kNone;
       if (lane < t.take) slot = verdict >= 0 ? static_cast<uint32_t>(verdict) + 2 : (verdict == -1 ? 0u : 1u);
       if (kHits == kKLdsHits) {
-        // denies / errors are common: one add per wave for them
-        const uint64_t dm = __ballot(slot == 0u), em = __ballot(slot == 1u);
-        if (lane == 0 && dm) atomicAdd(ctr, static_cast<uint32_t>(__popcll(dm)));
-        if (lane == 0 && em) atomicAdd(ctr + 1, static_cast<uint32_t>(__popcll(em)));
-        if (slot != kNone && slot >= 2u) atomicAdd(ctr + slot, 1u);
+        if (slot != kNone) atomicAdd(ctr + slot, 1u);
       } else {
         count_slot(hits, slot, slot != kNone);
       }

@@ -1145,13 +1145,10 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
                                            16, 0, 2);
       }
     } else {
-      const uint32_t qlast = t.bytes ? (t.bytes - 1u) / 16u : 0u;
 #pragma unroll
       for (uint32_t it = 0; it < kCopyIters; ++it) {
         const uint32_t q = it * 64u + lane;
-        // unconditional (no exec-mask branch per piece): lanes past the window
-        // load its last piece again (same line, no extra traffic)
-        if (t.bytes) buf[it] = __builtin_nontemporal_load(src + (q < qlast ? q : qlast));
+        if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
       }
     }
   };
@@ -1167,12 +1164,7 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
 #pragma unroll
       for (uint32_t it = 0; it < kCopyIters; ++it) {
         const uint32_t q = it * 64u + lane;
-        // whole pieces inside the stage: a uniform test, no exec-mask branch
-        if (it * 1024u + 1024u <= stage) {
-          if (t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
-        } else if (q * 16u < t.bytes) {
-          reinterpret_cast<u32x4*>(stg)[q] = buf[it];
-        }
+        if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
       }
     }
     wave_sync();
