@@ -82,8 +82,9 @@ struct DfaDesc {
   uint32_t acc_cmap_off; // kDfaSearch: program word offset of the 256-byte byte -> class map
   uint32_t acc_mid_off;  // kDfaSearch: program: u32 pattern mask per mid-set id (256)
   uint32_t acc_ncls;     // kDfaSearch: byte classes (row length of the dense table)
+  uint32_t pad[4];       // 128 bytes: descriptor addresses are a shift of the DFA index
 };
-static_assert(sizeof(DfaDesc) == 112, "dfa desc is 28 words");
+static_assert(sizeof(DfaDesc) == 128, "dfa desc is 32 words");
 
 // Search automata (L7M_DIALECT_RE2_SEARCH regex fields, Go regexp
 // MatchString): a dense DFA of [\x00-\xff]*(p0|...|pk), k < 32, walked as

@@ -28,7 +28,7 @@ DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_
 SKIP_LOOP, SKIP_LIT = 1, 2  # program.h kSkipLoop / kSkipLit
 SKIP_MIN_REST = 64  # l7m_kernels.hip kSkipMinRest: bytes left for a skip row to be taken
 ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
-DFA_WORDS = 28  # sizeof(DfaDesc) / 4
+DFA_WORDS = 32  # sizeof(DfaDesc) / 4
 DFA_SEARCH = 1  # program.h kDfaSearch
 
 
