@@ -281,6 +281,7 @@ struct LdsChain {
     // 8-byte blocks (the dead state is absorbing: one exit test per block);
     // a row with a skip descriptor is handled at the block boundary (slim =
     // ~0u without descriptors: never)
+#ifdef L7M_SKIP
     while (k + 8 <= len) {
       const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
       const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
@@ -321,6 +322,9 @@ struct LdsChain {
         if (k + 2 < len) L7M_STEP(src.byte(pos + k + 2))
       }
     }
+#else
+    L7M_WALK_BYTES(L7M_STEP, dead_now())
+#endif
 #undef L7M_STEP
   }
   __device__ __forceinline__ uint32_t code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
@@ -614,9 +618,11 @@ struct WalkOut {
   uint64_t present;   // fields present in the request
   uint32_t ex, e0;    // port entries whose rules may decide (exact port, port 0)
   uint32_t remote;    // the request's remote identity
-  uint32_t pf_t;      // the candidate-entry touch (kept live until the entry load)
+  uint32_t pf_t;      // the candidate-entry touch (kept live until verification)
+#ifdef L7M_EPF
   uint32_t pf_d;      // DFA whose candidate entry was touched, or kNone
   uint32_t pf_ent;    // that entry's word offset in the program, or kNone
+#endif
   bool h0;            // the port-0 entry has HTTP rules
 };
 constexpr int32_t kNeedVerify = INT32_MIN;
@@ -784,8 +790,13 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
   o.h0 = h0;
   o.remote = w1;
   o.pf_t = pf_t;
+#ifdef L7M_EPF
   o.pf_d = pf_d;
   o.pf_ent = pf_ent;
+#else
+  (void)pf_d;
+  (void)pf_ent;
+#endif
   return kNeedVerify;
 }
 
