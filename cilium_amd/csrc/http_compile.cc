@@ -754,6 +754,15 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     h.pres_fields_hi = static_cast<uint32_t>(pm >> 32);
   }
   h.n_policies = plan.n_policies;
+  // the kernel walks :path and :authority as two interleaved chains when each
+  // has exactly one automaton and both are walked from LDS
+  h.pair_pa = fd[kFieldPath].ndfa == 1 && fd[kFieldAuthority].ndfa == 1 &&
+                      dd[fd[kFieldPath].dfa_first].lds_table != kNone &&
+                      dd[fd[kFieldAuthority].dfa_first].lds_table != kNone &&
+                      dd[fd[kFieldPath].dfa_first].kind == kDfaPacked &&
+                      dd[fd[kFieldAuthority].dfa_first].kind == kDfaPacked
+                  ? 1u
+                  : 0u;
   for (uint32_t k = 0; k < ndfa; ++k) h.search |= dd[k].kind == kDfaSearch ? 1u : 0u;
   h.ent_mask = ent_slots - 1;
   h.ent_tab_off = take(2ull * ent_slots);

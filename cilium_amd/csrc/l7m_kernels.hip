@@ -710,6 +710,54 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
     }
   };
   for (uint32_t job = 0;; ++job) {
+#ifdef L7M_PAIR
+    // :path and :authority as two interleaved chains (h.pair_pa): their
+    // 8-byte blocks step together while both fields have one left, so each
+    // dependent LDS read overlaps the other chain's; the rests finish alone.
+    if (job == 1 && h.pair_pa) {
+      const uint32_t dP = c.fields[kFieldPath].dfa_first, dA = c.fields[kFieldAuthority].dfa_first;
+      const DfaDesc& ddP = c.dds[dP];
+      const DfaDesc& ddA = c.dds[dA];
+      const bool hasP = (flags & L7M_HTTP_F_PATH) != 0, hasA = (flags & L7M_HTTP_F_AUTHORITY) != 0;
+      const uint32_t posP = pos, posA = pos + plen;
+      const uint32_t lenP = ddP.start_base ? plen : 0u, lenA = ddA.start_base ? alen : 0u;
+      LdsChain cp, ca;
+      cp.init(ddP);
+      ca.init(ddA);
+      uint32_t kp = 0;
+      for (; kp + 4 <= lenP && kp + 4 <= lenA; kp += 4) {
+        const uint32_t p0 = src.byte(posP + kp), p1 = src.byte(posP + kp + 1), p2 = src.byte(posP + kp + 2),
+                       p3 = src.byte(posP + kp + 3);
+        const uint32_t a0 = src.byte(posA + kp), a1 = src.byte(posA + kp + 1), a2 = src.byte(posA + kp + 2),
+                       a3 = src.byte(posA + kp + 3);
+        cp.step(c.img, p0);
+        ca.step(c.img, a0);
+        cp.step(c.img, p1);
+        ca.step(c.img, a1);
+        cp.step(c.img, p2);
+        ca.step(c.img, a2);
+        cp.step(c.img, p3);
+        ca.step(c.img, a3);
+        if (cp.dead_now() && ca.dead_now()) {
+          kp += 4;
+          break;
+        }
+      }
+      if (lenP) cp.run(c.img, src, posP, lenP, kp < lenP ? kp : lenP);
+      if (lenA) ca.run(c.img, src, posA, lenA, kp < lenA ? kp : lenA);
+      const uint32_t codeP = hasP ? cp.code(c.img, c.prog, ddP) : 0u;
+      const uint32_t codeA = hasA ? ca.code(c.img, c.prog, ddA) : 0u;
+      if (hasP) present |= 1ull << kFieldPath;
+      if (hasA) present |= 1ull << kFieldAuthority;
+      codes.set(dP, codeP);
+      touch(dP, codeP);
+      codes.set(dA, codeA);
+      touch(dA, codeA);
+      pos += plen + alen;
+      ++job;  // the authority job is done
+      continue;
+    }
+#endif
     uint32_t f = kNone, p = pos, len = 0;
     if (job < 3) {
       len = job == 0 ? mlen : job == 1 ? plen : alen;

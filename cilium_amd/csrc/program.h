@@ -212,7 +212,8 @@ struct HttpHeader {
   uint32_t pres_fields_lo; // bit f: field f has a presence-keyed check-record list
   uint32_t pres_fields_hi;
   uint32_t search;         // 1: some value DFA is a kDfaSearch automaton (RE2 dialect)
-  uint32_t pad[3];         // header = 40 words
+  uint32_t pair_pa;        // 1: :path and :authority have one LDS-walked DFA each (paired walk)
+  uint32_t pad[2];         // header = 40 words
 };
 // Header-name table (LDS image): exact lower-case header names of the rules
 // -> field id, open addressing on the program.h name hash; slot =

@@ -21,7 +21,7 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
               "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi "
-              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search").split()
+              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search pair_pa").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab "
               "lds_skip skip_lim kind acc_cmap_off acc_mid_off acc_ncls").split()
@@ -54,7 +54,7 @@ class HttpProgram:
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
         h = self.h
         assert h["magic"] == 0x3448374C
-        assert len(HDR_FIELDS) == 37  # + 3 pad words (program.h HttpHeader, 40 words)
+        assert len(HDR_FIELDS) == 38  # + 2 pad words (program.h HttpHeader, 40 words)
         io = h["lds_image_off"]
         self.img = self.w[io:io + h["lds_image_words"]]
         self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
