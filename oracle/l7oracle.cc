@@ -1137,4 +1137,16 @@ int orc_kafka_eval_ids(void* h, const uint8_t* arena, size_t arena_bytes, const 
 
 void orc_kafka_free(void* h) { delete static_cast<KafkaOracle*>(h); }
 
+// proto/snappy.go snappyDecode of one value (framed or a bare block), for the
+// snappy known-answer tests: 0 decoded (out_len bytes into out), 1 the
+// reference returns an error (or panics), 2 out too small.
+int orc_snappy_decode(const uint8_t* src, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+  std::vector<uint8_t> d;
+  if (!go_snappy(std::string(reinterpret_cast<const char*>(src), n), &d)) return 1;
+  if (d.size() > cap) return 2;
+  if (!d.empty()) memcpy(out, d.data(), d.size());
+  *out_len = d.size();
+  return 0;
+}
+
 }  // extern "C"

@@ -40,3 +40,10 @@ extern "C" int kc_host_check_produce(const uint8_t* rec, uint32_t len, uint32_t 
   l7m::KcInflateScratch s;
   return l7m::kc_check_produce(rec, len, slab.data(), slab_bytes, tab, s);
 }
+
+// kc_unsnappy alone (framed or bare block): 0 decoded (*out_len bytes), 1
+// error, 2 over cap.  For the snappy known-answer tests.
+extern "C" int kc_host_unsnappy(const uint8_t* src, uint32_t n, uint8_t* out, uint32_t cap, uint32_t* out_len) {
+  const int rc = l7m::kc_unsnappy(src, n, out, cap, cap, out_len);
+  return rc == l7m::kCodecOk ? 0 : rc == l7m::kCodecErr ? 1 : 2;
+}

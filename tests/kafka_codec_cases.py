@@ -108,6 +108,16 @@ def value_cases():
     c.append(("snappy_bad_copy_offset", K.SNAPPY, K._uvarint(8) + bytes([0x0C, 0x61, 0x1E, 0x05, 0x00]), 1, -2))
     c.append(("snappy_decoded_over_maxParseBufSize", K.SNAPPY, K._uvarint(100 * 65535 + 1) + b"\0", 1, -2))
     c.append(("snappy_empty", K.SNAPPY, K._uvarint(0), 1, 0))
+    # every snappy element form, written by the format-description encoder
+    # (tests/test_snappy_spec_cpu.py pins both decoders on the bytes)
+    for nm, kw in (("copy1", dict(copy=1)), ("copy2_no_rle", dict(copy=2, rle=False)), ("copy4", dict(copy=4)),
+                   ("lit60", dict(copy=0, lit=60)), ("lit62", dict(copy=0, lit=62)),
+                   ("lit63_copy4", dict(copy=4, lit=63))):
+        c.append((f"snappy_forms_{nm}", K.SNAPPY, K.snappy_block_forms(INNER, **kw), 1, 0))
+    blk4 = K.snappy_block_forms(INNER, copy=4)
+    c.append(("snappy_java_forms_copy4", K.SNAPPY,
+              b"\x82SNAPPY\x00" + struct.pack(">II", 1, 1) + struct.pack(">I", len(blk4)) + blk4, 1, 0))
+    c.append(("snappy_forms_copy4_cut", K.SNAPPY, blk4[:-2], 1, -2))
     return c
 
 

@@ -255,6 +255,91 @@ def snappy_block(data):
     return bytes(out)
 
 
+def snappy_block_forms(data, lit=None, copy=1, rle=True):
+    """A snappy block of `data` written element by element from the snappy
+    format description, with chosen element forms (an encoder independent of
+    golang/snappy's, for pinning both decoders on every tag form):
+      lit   None: shortest literal tag; 60-63: every literal's length-1 in
+            1-4 bytes after the tag (longer literals split to fit);
+      copy  1: tag 01 (length 4-11, 11-bit offset) where it fits, else tag 10;
+            2: tag 10 (16-bit offset); 4: tag 11 (32-bit offset); 0: none;
+      rle   runs of one byte are written as an overlapping offset-1 copy."""
+    out = bytearray(_uvarint(len(data)))
+
+    def emit_literal(chunk):
+        cap = 1 << 16 if lit is None else 1 << (8 * (lit - 59))
+        for a in range(0, len(chunk), cap):
+            piece = chunk[a:a + cap]
+            n = len(piece) - 1
+            if lit is None and n < 60:
+                out.append(n << 2)
+            else:
+                k = (lit - 59) if lit is not None else max(1, (n.bit_length() + 7) // 8)
+                out.append((59 + k) << 2)
+                out.extend(n.to_bytes(k, "little"))
+            out.extend(piece)
+
+    def emit_copy(off, m):  # 1 <= m <= 64
+        if copy == 1 and 4 <= m <= 11 and off < 2048:
+            out.extend([((off >> 8) << 5) | ((m - 4) << 2) | 1, off & 0xFF])
+        elif copy in (1, 2):
+            out.append(((m - 1) << 2) | 2)
+            out.extend(off.to_bytes(2, "little"))
+        else:
+            out.append(((m - 1) << 2) | 3)
+            out.extend(off.to_bytes(4, "little"))
+
+    table, i, start = {}, 0, 0
+    while i < len(data):
+        best = None
+        if copy and rle and i >= 1:
+            m = 0
+            while i + m < len(data) and m < 64 and data[i + m] == data[i - 1]:
+                m += 1
+            if m >= 4:
+                best = (1, m)
+        if copy and best is None and i + 4 <= len(data):
+            j = table.get(bytes(data[i:i + 4]))
+            if j is not None and i - j < (1 << 16):
+                m = 4
+                while i + m < len(data) and m < 64 and data[j + m] == data[i + m]:
+                    m += 1
+                best = (i - j, m)
+        if i + 4 <= len(data):
+            table[bytes(data[i:i + 4])] = i
+        if best:
+            emit_literal(data[start:i])
+            emit_copy(*best)
+            i += best[1]
+            start = i
+        else:
+            i += 1
+    emit_literal(data[start:])
+    return bytes(out)
+
+
+def snappy_tags(block):
+    """Element tags of a snappy block, in order: 'lit<n>' (n = extra length
+    bytes, 0 inline) and 'copy1' / 'copy2' / 'copy4'."""
+    p = 0
+    while block[p] & 0x80:
+        p += 1
+    p += 1
+    tags = []
+    while p < len(block):
+        t = block[p] & 3
+        if t == 0:
+            x = block[p] >> 2
+            k = x - 59 if x >= 60 else 0
+            n = (int.from_bytes(block[p + 1:p + 1 + k], "little") if k else x) + 1
+            tags.append(f"lit{k}")
+            p += 1 + k + n
+        else:
+            tags.append(("copy1", "copy2", "copy4")[t - 1])
+            p += (2, 3, 5)[t - 1]
+    return tags
+
+
 def snappy_java(data, chunk=1024, version=1):
     """snappy-java framing (proto/snappy.go): magic, version, compat, chunks."""
     out = b"\x82SNAPPY\x00" + struct.pack(">II", version, 1)

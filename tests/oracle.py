@@ -35,6 +35,7 @@ def _load():
     lib.orc_kafka_new.argtypes = [ctypes.POINTER(L._KafkaRule), sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.orc_kafka_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_kafka_free.argtypes = [P]
+    lib.orc_snappy_decode.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     lib.orc_kafka_new_map.argtypes = [ctypes.POINTER(L._KafkaSelectorRules), sz, ctypes.POINTER(L._IdentitySelectors),
                                       sz, ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.orc_kafka_eval_ids.argtypes = [P, P, sz, P, sz, P, P, ctypes.c_int]
@@ -173,3 +174,12 @@ def regex_search(pattern: str, value: bytes) -> int:
 def nfa_match(pattern: str, value: bytes, search: bool = False) -> int:
     """The oracle's NFA simulator (oracle/nfa.h): 1/0, -1 syntax error, -2 unsupported."""
     return _lib.orc_nfa_match(pattern.encode(), value, len(value), 1 if search else 0)
+
+
+def snappy_decode(src: bytes, cap: int = 1 << 22):
+    """proto/snappy.go snappyDecode restated (oracle/l7oracle.cc go_snappy):
+    (0, decoded bytes), or (1, None) where the reference errors or panics."""
+    out = ctypes.create_string_buffer(max(cap, 1))
+    n = ctypes.c_size_t(0)
+    rc = _lib.orc_snappy_decode(src, len(src), out, cap, ctypes.byref(n))
+    return (rc, out.raw[:n.value] if rc == 0 else None)
