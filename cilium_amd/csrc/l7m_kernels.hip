@@ -710,6 +710,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
     }
   };
   for (uint32_t job = 0;; ++job) {
+    HPROF(4);  // (diagnostic build) what followed the previous job's walks
 #ifdef L7M_PAIR
     // :path and :authority as two interleaved chains (h.pair_pa): their
     // 8-byte blocks step together while both fields have one left, so each
@@ -813,12 +814,14 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
       }
     }
 #else
+    HPROF(2);  // job selection, header-name lookup
     if (f != kNone) {
       present |= 1ull << f;
       const FieldDesc& fd = c.fields[f];
       for (uint32_t k = 0; k < fd.ndfa; ++k) {
         const uint32_t d = fd.dfa_first + k;
         const uint32_t code = walk_dfa<kLit, (kReg < 0)>(c, d, src, p, len);
+        HPROF(3);  // the walk, end code included
         codes.set(d, code);
         touch(d, code);
       }
@@ -1341,7 +1344,7 @@ __global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __res
         prof[q] = o2 > prof[q] ? o2 : prof[q];
       }
     if (lane == 0)
-      printf("L7M_PROF validate %llu method %llu path %llu authority %llu headers %llu verify %llu eval %llu\n",
+      printf("L7M_PROF validate %llu jobsel %llu walks %llu setcode %llu tail %llu verify %llu eval %llu\n",
              (unsigned long long)prof[1], (unsigned long long)prof[2], (unsigned long long)prof[3],
              (unsigned long long)prof[4], (unsigned long long)prof[5], (unsigned long long)prof[6],
              (unsigned long long)prof[7]);
