@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/pmc_${1:-r01}
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--requests ${REQS:-8000000} --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+ARGS="--requests ${REQS:-8000000} --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-batcher ${BENCH_ARGS:-}"
 if [ "${LIST:-0}" = 1 ]; then
   timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1; echo "list rc=$?"
 fi
