@@ -606,15 +606,15 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   const uint32_t lds_name_field = img_take(name_field.size());
   {
     const uint64_t fixed = 4 * img + codes_bytes + ctr_bytes + stage_bytes;
-    if (fixed > kLdsBytes)
+    if (fixed > kHttpLdsBytes)
       return fail(L7M_ETOOBIG, std::to_string(ndfa) + " value DFA groups over " + std::to_string(nf) +
                                    " fields need " + std::to_string(fixed) + " bytes of fixed LDS (descriptors, "
-                                   "end-code columns, counters, record stage) > " + std::to_string(kLdsBytes));
+                                   "end-code columns, counters, record stage) > " + std::to_string(kHttpLdsBytes));
   }
   uint64_t budget_bytes = opts.lds_budget_bytes ? opts.lds_budget_bytes : kDefaultLdsBudget;
   {
     const uint64_t fixed = codes_bytes + ctr_bytes + stage_bytes;
-    budget_bytes = std::min<uint64_t>(budget_bytes, fixed < kLdsBytes ? kLdsBytes - fixed : 0);
+    budget_bytes = std::min<uint64_t>(budget_bytes, fixed < kHttpLdsBytes ? kHttpLdsBytes - fixed : 0);
   }
   const uint64_t budget = budget_bytes / 4;
   // header-name table (always resident when it fits)

@@ -1071,8 +1071,14 @@ enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
 // kLit: the program has literal tables (DfaDesc::lit_tab) for HBM-walked
 // DFAs; a separate instantiation, so programs without them keep the leaner
 // walk code.
+#if L7M_HTTP_WG_PER_CU > 1
+// (experiment) several workgroups per CU: the register budget of their waves
+#define L7M_HTTP_OCC __attribute__((amdgpu_waves_per_eu(L7M_HTTP_WG_PER_CU * L7M_HTTP_WAVES / 4)))
+#else
+#define L7M_HTTP_OCC
+#endif
 template <int kHits, int kReg, int kAblate, bool kLit>
-__global__ __launch_bounds__(kBlock) void http_eval_kernel(const uint32_t* __restrict__ prog,
+__global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const uint32_t* __restrict__ prog,
                                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                            const uint64_t* __restrict__ offs, uint64_t n,
                                                            int32_t* __restrict__ verdicts,
@@ -1369,8 +1375,8 @@ size_t http_lds_bytes(const HttpHeader& h, uint32_t stage) {
 // Bytes of records staged per wave: what is left of the LDS after the tables.
 uint32_t http_stage_bytes(const HttpHeader& h) {
   const size_t fixed = http_lds_bytes(h, 0) - kWaves * 16u;
-  if (fixed + kWaves * (256u + 16u) > kLdsBytes) return 0;
-  size_t s = (kLdsBytes - fixed) / kWaves - 16u;
+  if (fixed + kWaves * (256u + 16u) > kHttpLdsBytes) return 0;
+  size_t s = (kHttpLdsBytes - fixed) / kWaves - 16u;
   s &= ~size_t(15);
   return static_cast<uint32_t>(s > kMaxStage ? kMaxStage : s);
 }
@@ -1382,7 +1388,7 @@ static hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const ui
   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU); set per device
   // and instantiation, thread-safely (l7m_device.h)
   const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate, kLit>),
-                                         kLdsBytes);
+                                         kHttpLdsBytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate, kLit>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
                      offs, n, verdicts, hits, stage, scratch);
@@ -1396,8 +1402,9 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   const uint32_t stage = http_stage_bytes(h);
   if (stage == 0) return hipErrorInvalidValue;
   const size_t lds = http_lds_bytes(h, stage);
-  // One resident workgroup per CU; fewer for small batches (>= 8 records per wave).
-  uint64_t blocks = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256);
+  // kHttpWgPerCu resident workgroups per CU (1 by default); fewer for small
+  // batches (>= 8 records per wave).
+  uint64_t blocks = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * kHttpWgPerCu;
   const uint64_t want = (n + 8 * kBlock - 1) / (8 * kBlock);
   if (want < blocks) blocks = want;
   const dim3 grid(static_cast<uint32_t>(blocks));

@@ -133,6 +133,11 @@ constexpr uint32_t kEs8Latched = 0xffu;
 constexpr uint32_t kHttpWaves = L7M_HTTP_WAVES;
 constexpr uint32_t kHttpBlock = 64 * kHttpWaves;
 constexpr uint32_t kLdsBytes = 160u * 1024u;     // gfx950 LDS per CU (one workgroup)
+#ifndef L7M_HTTP_WG_PER_CU
+#define L7M_HTTP_WG_PER_CU 1  // resident HTTP workgroups per CU, each with its own table image
+#endif
+constexpr uint32_t kHttpWgPerCu = L7M_HTTP_WG_PER_CU;
+constexpr uint32_t kHttpLdsBytes = kLdsBytes / kHttpWgPerCu;  // LDS of one HTTP workgroup
 constexpr uint32_t kHttpRegDfas = 8;             // <= 8 value DFAs: end codes in registers
 constexpr uint32_t kMaxLdsCounters = 8192;       // per-rule hit counters kept in LDS up to this
 constexpr uint32_t kHttpMinStage = 2048;         // smallest record stage per wave (bytes)
