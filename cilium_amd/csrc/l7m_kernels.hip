@@ -1184,19 +1184,21 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     t.take = t.k ? t.k : 1u;
     return t;
   };
-  // Staging.  Register staging (the default): the next tile's bytes are
-  // loaded into VGPRs after the walks and written to the stage at the top of
-  // the next iteration.  LDS-DMA staging (global_load_lds_dwordx4,
-  // non-temporal; the literal-table instantiation, or L7M_LDSDMA): the bytes
-  // go HBM -> the wave's stage with no VGPR destination and no ds_write pass
-  // (lane l of piece `it` lands at stage + it * 1 KiB + 16 l, the coalesced
-  // copy's own layout), issued after the walks, the stage's only readers.
-  // Measured: registers are 2 % faster on config 2; LDS-DMA removes the
-  // literal instantiation's VGPR spills (config 5 1.277 -> 1.266 ms).
-#ifdef L7M_LDSDMA
-  constexpr bool kDma = true;
-#else
+  // Staging.  LDS-DMA staging (the default: global_load_lds_dwordx4,
+  // non-temporal): the next tile's bytes go HBM -> the wave's stage with no
+  // VGPR destination and no ds_write pass (lane l of piece `it` lands at
+  // stage + it * 1 KiB + 16 l, the coalesced copy's own layout), issued after
+  // the walks, the stage's only readers.  Register staging (L7M_REGSTAGE,
+  // except for the literal-table instantiation, whose register-staged build
+  // spills): the bytes are loaded into VGPRs after the walks and written to
+  // the stage at the top of the next iteration.  Measured on the round-3
+  // kernel: LDS-DMA 3.47-3.49 vs 3.52 ms on config 2, 8.83 vs 8.93 on
+  // config 4 (128 -> 105 VGPRs); the early round-3 kernel measured the
+  // opposite (3.58 vs 3.51).
+#ifdef L7M_REGSTAGE
   constexpr bool kDma = kLit;
+#else
+  constexpr bool kDma = true;
 #endif
   u32x4 buf[kCopyIters];
   auto issue_bytes = [&](const Tile& t) {
