@@ -145,10 +145,13 @@ def e2e_leg(rs, arena_pinned, offs, n, passes=2):
         rs.eval(arena_pinned, offs, None)
     dt = (time.perf_counter() - t) / passes
     del verd
+    zc = bool(L._lib.l7m_host_mapped(arena_pinned.ctypes.data, ((arena_pinned.nbytes + 64) & ~3)))
     return {"verdicts_per_s": n / dt, "ms_per_batch": dt * 1e3, "host_GBps": arena_pinned.nbytes / dt / 1e9,
-            "requests": n, "passes": passes,
-            "path": "l7m_eval(pinned host arena): 64 MiB chunks, H2D on 2 streams overlapped with the kernel, "
-                    "D2H verdicts"}
+            "requests": n, "passes": passes, "zero_copy": zc,
+            "path": ("l7m_eval(pinned host arena): zero-copy, the kernel reads the device-mapped arena in place "
+                     "over PCIe; offsets H2D, verdicts D2H") if zc else
+                    ("l7m_eval(pinned host arena): 64 MiB chunks, H2D on 2 streams overlapped with the kernel, "
+                     "D2H verdicts")}
 
 
 def batcher_leg(cfg, seconds):

@@ -309,6 +309,37 @@ bool ascending(const uint64_t* offs, size_t n, size_t arena_bytes) {
   return n == 0 || offs[n - 1] < arena_bytes;
 }
 
+// Zero-copy: a host buffer the device can address (pinned by hipHostMalloc /
+// l7m_alloc_pinned, mapped into the device's address space) is read by the
+// kernels in place over PCIe instead of being copied first (config 2, 2 GB:
+// 54.7 GB/s against 36.5 GB/s for the chunked H2D pipeline,
+// tools/zero_copy_probe.py).  Returns the device address of [p, p + bytes)
+// only when the runtime reports that whole range inside ONE device-mapped
+// host allocation, else nullptr (the caller copies).  L7M_ZERO_COPY=0
+// disables it.
+const void* mapped_host_range(const void* p, size_t bytes) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("L7M_ZERO_COPY");
+    return !(e && e[0] == '0');
+  }();
+  if (!enabled || !p || !bytes) return nullptr;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error here
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, a.devicePointer) != hipSuccess || !base) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const auto d = reinterpret_cast<uintptr_t>(a.devicePointer), b = reinterpret_cast<uintptr_t>(base);
+  if (d < b || d - b > size || bytes > size - (d - b)) return nullptr;
+  return a.devicePointer;
+}
+
 int eval_pipelined(EvalCtx* c, const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
                    const uint64_t* offsets, size_t n, const uint32_t* ids, int32_t* verdicts, bool hits,
                    size_t abytes, size_t nctr, uint32_t flags) {
@@ -583,8 +614,29 @@ int l7m_eval_ids(const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes
   const size_t abytes = (arena_bytes + 64) & ~size_t(3);
   EvalCtx* c = acquire_ctx(dev);
   if (!c) return L7M_EDEVICE;
-  int rc = c->reserve(abytes, n, nctr, ids != nullptr);
-  if (rc == L7M_OK && arena_bytes >= 2 * kPipeChunkBytes && ascending(offsets, n, arena_bytes)) {
+  // zero-copy when the padded arena is device-mapped host memory (the
+  // kernels' aligned over-reads stay inside [arena, arena + abytes))
+  const void* za = (reinterpret_cast<uintptr_t>(arena) & 15) ? nullptr : mapped_host_range(arena, abytes);
+  int rc = c->reserve(za ? 0 : abytes, n, nctr, ids != nullptr);
+  if (rc == L7M_OK && za) {
+    const hipStream_t st = c->stream;
+    const void* zo = (reinterpret_cast<uintptr_t>(offsets) & 7) ? nullptr : mapped_host_range(offsets, n * 8);
+    const void* zi = ids && !(reinterpret_cast<uintptr_t>(ids) & 3) ? mapped_host_range(ids, n * 4) : nullptr;
+    bool ok = (zo || hipMemcpyAsync(c->offs, offsets, n * 8, hipMemcpyHostToDevice, st) == hipSuccess) &&
+              (!ids || zi || hipMemcpyAsync(c->ids, ids, n * 4, hipMemcpyHostToDevice, st) == hipSuccess) &&
+              (!hits || hipMemsetAsync(c->hits, 0, nctr * 8, st) == hipSuccess);
+    if (!ok) rc = L7M_EDEVICE;
+    if (rc == L7M_OK)
+      rc = launch(rs, za, arena_bytes, zo ? zo : c->offs, n, c->verd, hits ? c->hits : nullptr, st, flags,
+                  ids ? (zi ? zi : c->ids) : nullptr);
+    if (rc == L7M_OK && hipMemcpyAsync(verdicts, c->verd, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = L7M_EDEVICE;
+    if (rc == L7M_OK && hits && hipMemcpyAsync(c->hhost.data(), c->hits, nctr * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
+      rc = L7M_EDEVICE;
+    if (hipStreamSynchronize(st) != hipSuccess && rc == L7M_OK) rc = L7M_EDEVICE;
+    if (rc == L7M_OK && hits)
+      for (size_t i = 0; i < nctr; ++i) hits[i] += c->hhost[i];
+  } else if (rc == L7M_OK && arena_bytes >= 2 * kPipeChunkBytes && ascending(offsets, n, arena_bytes)) {
     rc = eval_pipelined(c, rs, arena, arena_bytes, offsets, n, ids, verdicts, hits != nullptr, abytes, nctr, flags);
     if (rc == L7M_OK && hits)
       for (size_t i = 0; i < nctr; ++i) hits[i] += c->hhost[i];
@@ -619,5 +671,7 @@ int l7m_alloc_pinned(size_t bytes, void** out) {
 void l7m_free_pinned(void* p) {
   if (p) (void)hipHostFree(p);
 }
+
+int l7m_host_mapped(const void* p, size_t bytes) { return mapped_host_range(p, bytes) ? 1 : 0; }
 
 }  // extern "C"

@@ -59,7 +59,7 @@ EXPORTED_SYMBOLS = (
     "l7m_compile_http", "l7m_compile_kafka", "l7m_retain", "l7m_release",
     "l7m_ruleset_get_info", "l7m_ruleset_program", "l7m_http_translate",
     "l7m_http_record_size", "l7m_pack_http", "l7m_eval", "l7m_eval_device",
-    "l7m_alloc_pinned", "l7m_free_pinned", "l7m_abi_version", "l7m_device_count",
+    "l7m_alloc_pinned", "l7m_free_pinned", "l7m_host_mapped", "l7m_abi_version", "l7m_device_count",
     "l7m_compile_http_policies", "l7m_ruleset_policy_index", "l7m_ruleset_rule_origin",
     "l7m_batcher_create", "l7m_batcher_set_ruleset", "l7m_batcher_eval", "l7m_batcher_eval_http",
     "l7m_batcher_stats", "l7m_batcher_destroy", "l7m_http_deny_body", "l7m_kafka_deny_response",
@@ -254,6 +254,7 @@ def _load() -> ctypes.CDLL:
     lib.l7m_eval.argtypes = [P, P, sz, P, sz, P, P, ctypes.c_uint32]
     lib.l7m_eval_device.argtypes = [P, P, sz, P, sz, P, P, P, ctypes.c_uint32]
     lib.l7m_alloc_pinned.argtypes = [sz, ctypes.POINTER(P)]
+    lib.l7m_host_mapped.argtypes = [P, sz]
     lib.l7m_free_pinned.argtypes = [P]
     lib.l7m_free_pinned.restype = None
     return lib

@@ -481,9 +481,15 @@ int64_t l7m_kafka_access_log(const uint8_t* arena, size_t arena_bytes, const uin
                              const int32_t* verdicts, l7m_kafka_log_record* out, size_t cap);
 size_t l7m_kafka_api_key_name(int16_t api_key, char* out, size_t cap);
 
-/* Pinned host memory helpers (cgo may not retain Go pointers across calls). */
+/* Pinned host memory helpers (cgo may not retain Go pointers across calls).
+ * l7m_eval on an arena in pinned, device-mapped memory whose padded range
+ * [arena, arena + arena_bytes + 64) lies inside one such allocation (16-byte
+ * aligned) runs the kernels on it in place over PCIe, with no staging copy
+ * (zero-copy; L7M_ZERO_COPY=0 in the environment disables it); other arenas
+ * are copied.  l7m_host_mapped(p, bytes) = 1 when [p, p + bytes) qualifies. */
 int l7m_alloc_pinned(size_t bytes, void** out);
 void l7m_free_pinned(void* p);
+int l7m_host_mapped(const void* p, size_t bytes);
 
 /* Library / device information. */
 int l7m_abi_version(void);
