@@ -184,16 +184,19 @@ def cpu_model():
 
 def measured_traffic(cfg):
     """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE
-    passes (tools/traffic.py) of THIS kernel build (matched by .so hash) on
-    the default workload; None when no such measurement exists."""
+    passes (tools/traffic.py) of THIS kernel build (matched by the .so hash,
+    or by the hash of its device code objects, cilium_amd/codehash.py) on the
+    default workload; None when no such measurement exists."""
     import glob
     import hashlib
+    from cilium_amd.codehash import kernel_md5
     with open(L.LIB_PATH, "rb") as f:
         md5 = hashlib.md5(f.read()).hexdigest()
+    kmd5 = kernel_md5(L.LIB_PATH)
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_cfg{cfg}.json")), reverse=True):
         with open(path) as f:
             t = json.load(f)
-        if t.get("so_md5") == md5:
+        if t.get("so_md5") == md5 or t.get("kernel_md5") == kmd5:
             return float(t["traffic_bytes"])
     return None
 
