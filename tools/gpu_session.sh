@@ -24,9 +24,9 @@ for s in "$@"; do
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench:*) step bench_${s#bench:} 600 python -u bench.py --config ${s#bench:} || exit $? ;;
     benchq:*) step benchq_${s#benchq:} 600 python -u bench.py --config ${s#benchq:} --no-cpu-baseline || exit $? ;;
-    prof:*) c=${s#prof:}; step prof_$c 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_$c -o run --output-format csv -- python3 -u bench.py --config $c --steps 20 --warmup 2 --no-cpu-baseline || exit $? ;;
+    prof:*) c=${s#prof:}; step prof_$c 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof_$c -o run --output-format csv -- python3 -u bench.py --config $c --steps 20 --warmup 2 --no-cpu-baseline --no-e2e --no-batcher || exit $? ;;
     pmc:*) c=${s#pmc:}; cfg=${c%%:*}; ctr=${c#*:}
-           step pmc_${cfg}_$ctr 300 rocprofv3 --pmc $ctr -d $PWD/$OUT/pmc_${cfg}_$ctr -o run --output-format csv -- python3 -u bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline || exit $? ;;
+           step pmc_${cfg}_$ctr 300 rocprofv3 --pmc $ctr -d $PWD/$OUT/pmc_${cfg}_$ctr -o run --output-format csv -- python3 -u bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-batcher || exit $? ;;
     vtests:*) v=${s#vtests:}; name=${v%%:*}; kx=${v#*:}
            L7M_LIB=variants/$name.so step vtests_$name 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$kx"
            rc=$?; [ $rc -le 1 ] || exit $rc ;;
