@@ -16,3 +16,28 @@ def test_c_harness_links_and_fails_without_device(tmp_path):
     p, _ = run(str(tmp_path), rules, arena, offs, threads=2, iters=1)
     assert p.returncode == 1
     assert "l7m_eval -6" in p.stderr
+
+
+def test_kernel_code_hash_covers_both_kernel_objects():
+    """bench.py keys measured traffic on the device code objects' hash
+    (cilium_amd/codehash.py): the library holds the HTTP and the Kafka gfx950
+    code objects, and the hash is stable and differs from the file hash."""
+    import hashlib
+    import struct
+    from cilium_amd import l7match as L
+    from cilium_amd.codehash import kernel_md5, _MAGIC
+    data = open(L.LIB_PATH, "rb").read()
+    n_gfx = 0
+    i = 0
+    while (j := data.find(_MAGIC, i)) >= 0:
+        n = struct.unpack_from("<Q", data, j + len(_MAGIC))[0]
+        p = j + len(_MAGIC) + 8
+        for _ in range(n):
+            _, size, idlen = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            n_gfx += b"gfx950" in data[p:p + idlen] and size > 0
+            p += idlen
+        i = j + 1
+    assert n_gfx == 2
+    k = kernel_md5(L.LIB_PATH)
+    assert k == kernel_md5(L.LIB_PATH) and k != hashlib.md5(data).hexdigest()
