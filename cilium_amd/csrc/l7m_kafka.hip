@@ -942,7 +942,7 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   if (stage > kKMaxStage) stage = kKMaxStage;
   const size_t lds = fixed + kKWaves * (stage + 16u);
   uint64_t blocks = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256);
-  const uint64_t want = (n + 8 * kKBlock - 1) / (8 * kKBlock);
+  const uint64_t want = (n + 2 * kKBlock - 1) / (2 * kKBlock);
   if (want < blocks) blocks = want;
   const dim3 grid(static_cast<uint32_t>(blocks));
   const uint32_t st = static_cast<uint32_t>(stage);

@@ -1405,9 +1405,9 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   if (stage == 0) return hipErrorInvalidValue;
   const size_t lds = http_lds_bytes(h, stage);
   // kHttpWgPerCu resident workgroups per CU (1 by default); fewer for small
-  // batches (>= 8 records per wave).
+  // batches (>= 2 records per lane, two tiles per wave).
   uint64_t blocks = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * kHttpWgPerCu;
-  const uint64_t want = (n + 8 * kBlock - 1) / (8 * kBlock);
+  const uint64_t want = (n + 2 * kBlock - 1) / (2 * kBlock);
   if (want < blocks) blocks = want;
   const dim3 grid(static_cast<uint32_t>(blocks));
   const bool reg = h.n_dfas <= kRegDfas;
