@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned-host end-to-end leg")
     ap.add_argument("--no-batcher", action="store_true", help="skip the per-request batcher leg")
     ap.add_argument("--batcher-seconds", type=float, default=3.0)
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle sample of the timed batch")
+    ap.add_argument("--parity-sample", type=int, default=200_000, help="requests of the timed batch checked")
     return ap.parse_args()
 
 
@@ -131,6 +133,43 @@ def cpu_baseline(cfg, rules, seconds, threads):
                       f"on {threads} threads = every core this process can use (affinity {hc['affinity']} CPUs, "
                       f"nproc {hc['nproc']}, cgroup CPU quota {hc['cgroup_quota_cores']} cores); "
                       f"single_thread_value: the first {len(o1)} of them on 1 thread, {dt1:.1f} s"}
+
+
+def parity_leg(cfg, rules, verdicts, lo, n, threads, n_sample=200_000, blocks=256, seed=None, n_rules=None):
+    """The timed batch's own verdicts against the oracle (test infrastructure,
+    outside the timed region): `blocks` contiguous runs of requests spread
+    evenly over this rank's shard [lo, lo + n), n_sample requests in all (the
+    whole shard when it is smaller), regenerated on the host (request i
+    depends only on (config, seed, i)) and evaluated by oracle/l7oracle.cc;
+    config 5 with its NFA engine (std::regex cannot run its long subjects)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import HttpOracle, KafkaOracle  # test infrastructure: the checker
+    gcfg = cfg
+    proto = W.CONFIGS[gcfg]["proto"]
+    engine = "nfa" if cfg == 5 else "std"
+    t0 = time.perf_counter()
+    orc = HttpOracle(rules, engine=engine) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+    if n <= n_sample:
+        runs = [(0, n)]
+    else:
+        b = -(-n_sample // blocks)
+        runs = [((n - b) * j // (blocks - 1), b) for j in range(blocks)]
+    sampled = mism = 0
+    first = None
+    for start, cnt in runs:
+        a, o = W.requests(gcfg, lo + start, cnt, seed=seed, n_rules=n_rules if n_rules else len(rules),
+                          threads=min(threads, 16))
+        exp = orc.eval(a, o, threads=threads)
+        got = verdicts[start:start + cnt]
+        bad = np.nonzero(got != exp)[0]
+        if len(bad) and first is None:
+            first = {"request": int(lo + start + bad[0]), "gpu": int(got[bad[0]]), "oracle": int(exp[bad[0]])}
+        sampled += cnt
+        mism += len(bad)
+    return {"sampled": sampled, "mismatches": mism, "runs": len(runs), "first_mismatch": first,
+            "oracle": f"oracle/l7oracle.cc ({'NFA engine' if engine == 'nfa' else 'std::regex' if proto == L.PROTO_HTTP else 'ReadRequest + MatchesRule'})",
+            "sample": f"{len(runs)} evenly spaced runs of {runs[0][1]} requests over this rank's shard of the timed "
+                      f"batch (last timed step's verdicts)", "seconds": time.perf_counter() - t0}
 
 
 def e2e_leg(rs, arena_pinned, offs, n, passes=2):
@@ -334,6 +373,11 @@ def main():
             "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
         }
         log(f"timed {args.steps} steps: {elapsed:.3f} s; kernel {kavg * 1e3:.2f} ms")
+        if not args.no_parity and not args.diag:
+            log("parity sample (oracle, outside the timed region)")
+            res["parity"] = parity_leg(cfg, rules, d_verd.cpu().numpy(), lo, per_gpu,
+                                       args.threads or host_cores()["usable"], n_sample=args.parity_sample)
+            log(f"parity: {res['parity']['mismatches']} mismatches in {res['parity']['sampled']}")
         if keep_host:
             log("end-to-end (pinned host arena)")
             res["e2e"] = e2e_leg(rs, pinned.numpy(), host_offs, per_gpu)
@@ -375,7 +419,7 @@ def run_mixed(args, world, rank, dev, scaling):
         arena, offs = W.requests(gcfg, lo, hi - lo, seed=seed, n_rules=n_rules, threads=threads)
         d_arena = torch.from_numpy(arena).to(dev)
         d_offs = torch.from_numpy(offs.view(np.int64)).to(dev)
-        parts.append(dict(proto=proto, gcfg=gcfg, rules=rules, rs=rs, n=hi - lo, seed=seed,
+        parts.append(dict(proto=proto, gcfg=gcfg, rules=rules, rs=rs, n=hi - lo, lo=lo, seed=seed,
                           arena_nbytes=arena.nbytes, rec_bytes=arena.nbytes - 64, d_arena=d_arena,
                           d_offs=d_offs, d_verd=torch.empty(hi - lo, dtype=torch.int32, device=dev),
                           stream=(torch.cuda.Stream(device=dev) if args.mixed_streams == 2
@@ -456,6 +500,12 @@ def run_mixed(args, world, rank, dev, scaling):
                      "note": "both kernels, first start to last end, rank 0"},
         "counters_ok": counters_ok,
     }
+    if not args.no_parity:
+        log("parity sample (oracle, outside the timed region)")
+        thr = args.threads or host_cores()["usable"]
+        res["parity"] = [dict(parity_leg(p["gcfg"], p["rules"], p["d_verd"].cpu().numpy(), p["lo"], p["n"], thr,
+                                         n_sample=args.parity_sample // 2, seed=p["seed"], n_rules=len(p["rules"])),
+                              part_config=p["gcfg"]) for p in parts]
     if world == 1 and not args.no_cpu_baseline:
         threads = args.threads or host_cores()["usable"]
         sys.path.insert(0, os.path.join(ROOT, "tests"))

@@ -594,7 +594,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   // (search programs keep their end codes in a global scratch, l7m_kernels.hip)
   const uint64_t codes_bytes = ndfa > kHttpRegDfas && !any_search ? 4ull * kHttpBlock * ndfa : 0;
   const uint64_t ctr_bytes = n + 2 <= kMaxLdsCounters ? 4ull * ((n + 2 + 3) & ~uint64_t(3)) : 0;
-  const uint64_t stage_bytes = static_cast<uint64_t>(kHttpWaves) * (kHttpMinStage + 16) + kHttpPrefetchSink;
+  const uint64_t stage_bytes = static_cast<uint64_t>(kHttpWaves) * (kHttpMinStage + 16);
   uint64_t img = 0;  // image words
   auto img_take = [&](uint64_t words) {
     uint64_t o = img;
@@ -681,18 +681,6 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       // once per walk) stay in the program
       dd[k].lds_table = img_take(d.n_slots);
     }
-    // skip descriptors (dfa_pack.h): the literal pool, then one word per
-    // skip-row base; only with the table in LDS and when they fit too
-    // (only for kernels built with L7M_SKIP: the descriptors cost image space,
-    // i.e. record stage, and the kernel's skip handler measured slower on
-    // config 2)
-    const uint64_t pool_words = ((d.skip_lits.size() + 3) / 4 + 3) & ~uint64_t(3);  // img_take granules
-    if (kSkipRowsInKernel && dd[k].lds_table != kNone && d.skip_lim && d.skip_lim < (1u << 16) &&
-        pool_words < (1u << 15) && img + pool_words + d.skip.size() + 8 <= budget) {
-      img_take(pool_words);
-      dd[k].lds_skip = img_take(d.skip.size());
-      dd[k].skip_lim = d.skip_lim | static_cast<uint32_t>(pool_words) << 16;
-    }
   }
   // Candidate tables are read once per request (after the walks), so they
   // only go to LDS while the image stays small: record staging space is worth
@@ -754,15 +742,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     h.pres_fields_hi = static_cast<uint32_t>(pm >> 32);
   }
   h.n_policies = plan.n_policies;
-  // the kernel walks :path and :authority as two interleaved chains when each
-  // has exactly one automaton and both are walked from LDS
-  h.pair_pa = fd[kFieldPath].ndfa == 1 && fd[kFieldAuthority].ndfa == 1 &&
-                      dd[fd[kFieldPath].dfa_first].lds_table != kNone &&
-                      dd[fd[kFieldAuthority].dfa_first].lds_table != kNone &&
-                      dd[fd[kFieldPath].dfa_first].kind == kDfaPacked &&
-                      dd[fd[kFieldAuthority].dfa_first].kind == kDfaPacked
-                  ? 1u
-                  : 0u;
+  h.pair_pa = 0;  // (unused; the paired walk measured slower, profiles/r03/ab_round3.md)
   for (uint32_t k = 0; k < ndfa; ++k) h.search |= dd[k].kind == kDfaSearch ? 1u : 0u;
   h.ent_mask = ent_slots - 1;
   h.ent_tab_off = take(2ull * ent_slots);
@@ -876,11 +856,6 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
                          : (t0 << kLdsRowShift);
       }
       if (in_entry && d.start_base) dd[k].start_es8 = es8(d.start_base);
-      if (dd[k].lds_skip != kNone) {
-        std::memcpy(I + dd[k].lds_skip, d.skip.data(), d.skip.size() * 4);
-        std::memcpy(reinterpret_cast<uint8_t*>(I + dd[k].lds_skip - (dd[k].skip_lim >> 16)), d.skip_lits.data(),
-                    d.skip_lits.size());
-      }
       for (uint32_t s = 0; dd[k].lds_es != kNone && !in_entry && s < d.n_slots; ++s)
         I16[dd[k].lds_es + s] = d.es[s] == kLatchedAccept ? static_cast<uint16_t>(kEs16Latched)
                                                            : static_cast<uint16_t>(d.es[s]);

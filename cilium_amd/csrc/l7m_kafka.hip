@@ -118,21 +118,7 @@ struct RdL {
   __device__ static __forceinline__ uint64_t be(Rd& d, uint32_t n) {
     const bool ok = !d.err && d.len - d.pos >= n;
     uint64_t v = 0;
-#ifdef L7M_KPERM
-    // big-endian field from the two aligned stage words holding it: one
-    // v_perm picks its bytes (records start 4-byte aligned in the stage)
-    if (n == 2 || n == 4) {
-      const uint32_t q = d.pos;
-      const uint32_t* a = reinterpret_cast<const uint32_t*>(d.p + (q & ~3u));
-      const uint32_t w0 = a[0], w1 = a[1], sh = q & 3u;
-      const uint32_t sel = n == 4 ? 0x00010203u + sh * 0x01010101u : 0x0c0c0001u + sh * 0x00000101u;
-      v = __builtin_amdgcn_perm(w1, w0, sel);
-    } else {
-      for (uint32_t i = 0; i < n; ++i) v = (v << 8) | d.p[d.pos + i];
-    }
-#else
     for (uint32_t i = 0; i < n; ++i) v = (v << 8) | d.p[d.pos + i];
-#endif
     d.err = !ok;
     d.pos = ok ? d.pos + n : d.len;
     return ok ? v : 0;
@@ -210,17 +196,12 @@ __device__ int read_message_set(Rd& d, int32_t size, int16_t version, const uint
   return rc;
 }
 
+// Diagnostic builds (L7M_PROF, kProf): per-lane cycle accumulators
+// (s_memtime): [0] start, [1] decode, [2] topic rounds, [3] ClientID, [4] eval.
 #ifdef L7M_PROF
-// Diagnostic build only: per-lane cycle accumulators (s_memtime).
-#define g_prof_t0 prof[0]
-#define g_prof_dec prof[1]
-#define g_prof_rounds prof[2]
-#define g_prof_client prof[3]
-#define PROF_PARAM , uint64_t (&prof)[5]
-#define PROF_ARG , prof
+constexpr bool kProf = true;
 #else
-#define PROF_PARAM
-#define PROF_ARG
+constexpr bool kProf = false;
 #endif
 
 struct KView {
@@ -403,10 +384,8 @@ constexpr uint32_t kTopicQ = 4;
 template <bool kLds>
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
                                               uint64_t limit, const uint32_t* crc_tab, uint16_t* tq,
-                                              uint64_t gmask, bool& comp PROF_PARAM) {
-#ifdef L7M_PROF
-  if (kLds) g_prof_t0 = __builtin_amdgcn_s_memtime();
-#endif
+                                              uint64_t gmask, bool& comp, uint64_t (&prof)[5]) {
+  if constexpr (kProf && kLds) prof[0] = __builtin_amdgcn_s_memtime();
   if (limit < 4) return L7M_VERDICT_PARSE_ERROR;
   const int32_t msize = static_cast<int32_t>((static_cast<uint32_t>(rec[0]) << 24) |
                                              (static_cast<uint32_t>(rec[1]) << 16) |
@@ -437,14 +416,10 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     uint32_t coff, clen;
     R::str(d, &coff, &clen);
     const uint8_t* client = rec + coff;
-#ifdef L7M_PROF
-    const uint64_t tc0 = __builtin_amdgcn_s_memtime();
-#endif
+    const uint64_t tc0 = kProf ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t cid = intern_client<kLds>(v, client, clen);
     const uint64_t kok = v.kind_ok[kidx];
-#ifdef L7M_PROF
-    if (kLds) g_prof_client += __builtin_amdgcn_s_memtime() - tc0;
-#endif
+    if constexpr (kProf && kLds) prof[3] += __builtin_amdgcn_s_memtime() - tc0;
 
     int32_t ntop = 0;
     bool ok = true;
@@ -550,49 +525,27 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     } else if (ntop == 0) {
       first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, true, cid, gmask);
     } else {
-#ifdef L7M_PROF
-      const uint64_t tr0 = __builtin_amdgcn_s_memtime();
-      if (kLds) g_prof_dec += tr0 - g_prof_t0;
-#endif
+      const uint64_t tr0 = kProf ? __builtin_amdgcn_s_memtime() : 0;
+      if constexpr (kProf && kLds) prof[1] += tr0 - prof[0];
       // The parked topics' home-slot heads (hash, meta, first rule) are
       // fetched together, so the lookups of a request cost one dependent
       // L2 round trip instead of one per topic; the second pass compares
       // names against the slots' inline prefixes (same cache line).
       uint32_t hs[kTopicQ];
       u32x4 hd[kTopicQ];
-#ifdef L7M_KSLOT32
-      u32x4 hp[kTopicQ];  // the slots' inline name prefixes, fetched with the heads
-#endif
 #pragma unroll
       for (uint32_t r = 0; r < kTopicQ; ++r) {
         hs[r] = 0;
         hd[r] = u32x4{0u, 0u, 0u, 0u};
-#ifdef L7M_KSLOT32
-        hp[r] = u32x4{0u, 0u, 0u, 0u};
-#endif
         if (r < nq && maxf != kNone) {
           const uint32_t toff = tq[64 * r];
           const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
           if (tlen && tlen <= kMaxTopicLen && v.n_slots) {
             hs[r] = load_name<kLds>(rec + toff, tlen).hash;
             hd[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[0];
-#ifdef L7M_KSLOT32
-            hp[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[1];
-#endif
           }
         }
       }
-#ifdef L7M_KPF2
-      // the home slots' inline name prefixes (same lines as the heads, L1
-      // hits by now), all requested before the first compare
-      u32x4 hp[kTopicQ];
-#pragma unroll
-      for (uint32_t r = 0; r < kTopicQ; ++r) {
-        hp[r] = u32x4{0u, 0u, 0u, 0u};
-        if (r < nq && maxf != kNone && hs[r] && hd[r].x != 0)
-          hp[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[1];
-      }
-#endif
 #pragma unroll
       for (uint32_t r = 0; r < kTopicQ; ++r) {
         if (r < nq && maxf != kNone) {
@@ -606,11 +559,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
             sl.meta = hd[r].y;
             sl.r0 = hd[r].z;
             sl.r0_client = hd[r].w;
-#if defined(L7M_KSLOT32) || defined(L7M_KPF2)
-            const u32x4 pf = hp[r];
-#else
             const u32x4 pf = reinterpret_cast<const u32x4*>(v.slots + at)[1];
-#endif
             sl.pfx[0] = pf.x;
             sl.pfx[1] = pf.y;
             sl.pfx[2] = pf.z;
@@ -623,9 +572,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       }
       const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid, gmask);
       first = j < maxf ? j : maxf;
-#ifdef L7M_PROF
-      if (kLds) g_prof_rounds += __builtin_amdgcn_s_memtime() - tr0;
-#endif
+      if constexpr (kProf && kLds) prof[2] += __builtin_amdgcn_s_memtime() - tr0;
     }
   }
   return first == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(first);
@@ -652,11 +599,6 @@ constexpr uint32_t kKMaxLdsCounters = 16384;
 constexpr uint32_t kSpanLds = (4 * kKafkaKinds + 3) & ~3u;  // words
 constexpr uint32_t kKindOkLds = (2 * kKafkaKinds + 3) & ~3u;  // words
 constexpr uint32_t kMaxCliLdsBytes = 8192;  // client table copied to LDS up to this size
-#ifdef L7M_KDMA
-constexpr uint32_t kKPrefetchSink = 256;  // LDS bytes of the next tile's L2 prefetch (64 lanes x 4)
-#else
-constexpr uint32_t kKPrefetchSink = 0;
-#endif
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t x, uint32_t src) {
   const uint32_t lo = __shfl(static_cast<uint32_t>(x), src);
@@ -689,9 +631,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
                                                              uint32_t* __restrict__ crecs, uint32_t* qhdr,
                                                              uint32_t qcap, const uint32_t* __restrict__ ids) {
   extern __shared__ __align__(16) uint32_t ksmem[];
-#ifdef L7M_PROF
-  uint64_t prof[5] = {0, 0, 0, 0, 0};
-#endif
+  uint64_t prof[5] = {0, 0, 0, 0, 0};  // (kProf diagnostic builds)
   const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t n_ctr = h.n_rules + 2;
@@ -703,12 +643,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   const uint32_t cli_words = kCliLds ? h.n_clients * (sizeof(KafkaClientSlot) / 4) : 0u;
   uint32_t* ctr = cli + cli_words;
   uint16_t* tq = reinterpret_cast<uint16_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
-#ifdef L7M_KDMA
-  uint8_t* pfz = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ);  // L2-prefetch sink (never read)
-  uint8_t* stg = pfz + kKPrefetchSink + wv * (stage + 16u);
-#else
   uint8_t* stg = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ) + wv * (stage + 16u);
-#endif
   tq += wv * 64 * kTopicQ + lane;
   if (kCliLds)
     for (uint32_t i = tid; i < cli_words; i += kKBlock) cli[i] = prog[h.off_clients + i];
@@ -769,26 +704,11 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     t.take = t.k ? t.k : 1u;
     return t;
   };
-#ifdef L7M_KDMA
-  // LDS-DMA staging (global_load_lds_dwordx4, non-temporal), issued after the
-  // tile's decode and lookups (the stage's only readers); the next tile's
-  // window is pulled into L2 at the top of the iteration (one 4-byte LDS-DMA
-  // per 128-byte line into a sink), so the copy waits for L2, not HBM, and
-  // no registers hold in-flight bytes through the decode.
-  auto issue_bytes = [&](const Tile& t) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's stage reads are done
-#pragma unroll
-    for (uint32_t it = 0; it < kKCopyIters; ++it) {
-      const uint32_t q = it * 64u + lane;
-      if (q * 16u < t.bytes)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
-                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                             reinterpret_cast<uintptr_t>(stg + it * 1024u)),
-                                         16, 0, 2);
-    }
-  };
-#else
+  // Register staging: the next tile's bytes are loaded into VGPRs at the top
+  // of the iteration and written to the stage at the top of the next one.
+  // (LDS-DMA staging issued after the lookups measured slower here: 4.30 vs
+  // 4.22 ms, profiles/r03/ab_round3.md: the decode alone does not cover the
+  // HBM latency.)
   u32x4 buf[kKCopyIters];
   auto issue_bytes = [&](const Tile& t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
@@ -798,23 +718,12 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
       if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
     }
   };
-#endif
   uint64_t o1, n1, o2, n2;
   load_offs(n * gw / nw, &o1, &n1);
   Tile t = plan(n * gw / nw, o1, n1);
   issue_bytes(t);
   load_offs(t.cur + t.take, &o2, &n2);
   while (t.cur < end) {
-#ifdef L7M_KDMA
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
-    wave_sync();
-    const Tile t2 = plan(t.cur + t.take, o2, n2);
-    if (lane * 128u < t2.bytes)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(arena + t2.base + lane * 128u),
-                                       reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                           reinterpret_cast<uintptr_t>(pfz)),
-                                       4, 0, 0);
-#else
 #pragma unroll
     for (uint32_t it = 0; it < kKCopyIters; ++it) {
       const uint32_t q = it * 64u + lane;
@@ -824,13 +733,10 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     const Tile t2 = plan(t.cur + t.take, o2, n2);
     issue_bytes(t2);
     load_offs(t2.cur + t2.take, &o2, &n2);
-#endif
 
     const uint64_t o = t.o, onext = t.onext;
     int32_t verdict = 0;
-#ifdef L7M_PROF
-    const uint64_t te0 = __builtin_amdgcn_s_memtime();
-#endif
+    const uint64_t te0 = kProf ? __builtin_amdgcn_s_memtime() : 0;
     // GetRelevantRules (pkg/policy/l4.go:110-129): the L7DataMap entries whose
     // rules apply to this request's source identity
     uint64_t gmask = ~0ull;
@@ -857,13 +763,13 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, gmask, comp PROF_ARG);
+          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, gmask, comp, prof);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, gmask, comp PROF_ARG)
+        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, gmask, comp, prof)
                       : L7M_VERDICT_PARSE_ERROR;
       }
       if (comp && verdict != L7M_VERDICT_PARSE_ERROR) {  // queue the request for the second pass
@@ -873,13 +779,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
       }
       verdicts[t.cur + lane] = verdict;
     }
-#ifdef L7M_KDMA
-    issue_bytes(t2);  // the stage's readers are done
-    load_offs(t2.cur + t2.take, &o2, &n2);
-#endif
-#ifdef L7M_PROF
-    prof[4] += __builtin_amdgcn_s_memtime() - te0;
-#endif
+    if constexpr (kProf) prof[4] += __builtin_amdgcn_s_memtime() - te0;
     if (kHits != kKNoHits) {
       uint32_t slot = kNone;
       if (lane < t.take) slot = verdict >= 0 ? static_cast<uint32_t>(verdict) + 2 : (verdict == -1 ? 0u : 1u);
@@ -892,8 +792,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     wave_sync();  // the stage is overwritten by the next tile
     t = t2;
   }
-#ifdef L7M_PROF
-  if (blockIdx.x == 0 && wv == 0) {
+  if (kProf && blockIdx.x == 0 && wv == 0) {
     for (int k = 0; k < 5; ++k)
       for (uint32_t m = 1; m < 64; m <<= 1) {
         const uint64_t o2 = shfl64(prof[k], lane ^ m);
@@ -903,7 +802,6 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
       printf("L7M_PROF decode %llu client %llu rounds %llu eval %llu\n", (unsigned long long)prof[1],
              (unsigned long long)prof[3], (unsigned long long)prof[2], (unsigned long long)prof[4]);
   }
-#endif
   if (kHits == kKLdsHits) {
     __syncthreads();
     for (uint32_t i = tid; i < n_ctr; i += kKBlock)
@@ -936,7 +834,7 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const bool cli_lds = cli_words && cli_words * 4 <= kMaxCliLdsBytes;
   const size_t fixed = 4u * (256u + kSpanLds + kKindOkLds + (cli_lds ? cli_words : 0u) +
                              (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
-                       2u * kKWaves * 64 * kTopicQ + kKPrefetchSink;
+                       2u * kKWaves * 64 * kTopicQ;
   size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
   stage &= ~size_t(15);
   if (stage > kKMaxStage) stage = kKMaxStage;

@@ -36,8 +36,12 @@ constexpr uint32_t kWaves = kHttpWaves;
 constexpr uint32_t kBlock = kHttpBlock;
 constexpr uint32_t kMaxStage = kHttpMaxStage;  // bytes of records staged per wave and tile
 constexpr uint32_t kCopyIters = kMaxStage / 1024;
-constexpr uint32_t kPrefetchSink = kHttpPrefetchSink;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#ifdef L7M_PROF
+constexpr bool kProf = true;  // diagnostic build: wave timeline printed by two waves
+#else
+constexpr bool kProf = false;
+#endif
 
 // Explicit address-space loads where one expression picks between an LDS
 // word and a program word: left generic, the compiler merges the two into a
@@ -202,67 +206,13 @@ __device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, c
 //     slot = (sel >> 16) + b;  e = img[slot];  sel = label(e) == b ? e : dead
 // with the word / byte selects folded into SDWA operands.  `slast` is the
 // slot of the last transition taken from a multi-pattern row (below lim).
-constexpr uint32_t kSkipMinRest = 64;  // bytes left in the field for a skip descriptor to be taken
-
 struct LdsChain {
   uint32_t sel, dead, lim, slast;
-  uint32_t slim;  // rows >= slim carry skip descriptors (dfa_pack.h), ~0u: none
-  uint32_t sk;    // LDS word of the descriptor of row slim
-  uint32_t lw;    // LDS word of the literal pool
   __device__ __forceinline__ void init(const DfaDesc& dd) {
     dead = dd.lds_table << kLdsRowShift;
     lim = dd.lds_table + dd.region;
     sel = ((dd.lds_table + dd.start_base) << kLdsRowShift) | (dd.start_es8 << 8);
     slast = kNone;
-#ifdef L7M_SKIP
-    slim = dd.lds_skip != kNone ? dd.lds_table + (dd.skip_lim & 0xffffu) : ~0u;
-    sk = dd.lds_skip;
-    lw = dd.lds_skip - (dd.skip_lim >> 16);
-#else
-    slim = ~0u;
-    sk = lw = 0;
-#endif
-  }
-  // Skip rows (latched, so slast is unaffected): a loop row decides the rest
-  // of the field with independent lookups; a literal run is compared with
-  // its bytes and the walk jumps past it.  Called for lanes whose row is
-  // >= slim at a block boundary; returns the new k (len when decided).
-  template <class Src>
-  __device__ __forceinline__ uint32_t skip(const uint32_t* __restrict__ img, const Src& src, uint32_t pos, uint32_t len,
-                                        uint32_t k) {
-    const uint32_t t0 = dead >> kLdsRowShift;
-    for (uint32_t guard = 0; guard < 64; ++guard) {
-      const uint32_t row = sel >> kLdsRowShift;
-      if (row < slim || sel == dead || k >= len) return k;
-      const uint32_t w = img[sk + (row - slim)];
-      if (w & kSkipLoop) {  // every byte must be one of the row's own labels
-        uint32_t bad = 0;
-#pragma nounroll
-        for (; k < len; ++k) {
-          const uint32_t b = src.byte(pos + k);
-          bad |= (img[row + b] ^ b) & 0xffu;
-        }
-        if (bad) sel = dead;
-        return len;
-      }
-      if (!(w & kSkipLit)) return k;
-      const uint32_t n = (w >> 2) & 31u, off = (w >> 7) & 511u;
-      if (len - k < n) {  // ends inside the literal run (non-accepting rows)
-        sel = dead;
-        return len;
-      }
-      uint32_t x = 0;
-      const uint8_t* L = reinterpret_cast<const uint8_t*>(img + lw);
-#pragma nounroll
-      for (uint32_t i = 0; i < n; ++i) x |= src.byte(pos + k + i) ^ L[off + i];
-      if (x) {
-        sel = dead;
-        return len;
-      }
-      sel = img[t0 + (w >> 16)];
-      k += n;
-    }
-    return k;
   }
   __device__ __forceinline__ void step(const uint32_t* __restrict__ img, uint32_t b) {
     uint32_t s = (sel >> kLdsRowShift) + b;
@@ -272,59 +222,12 @@ struct LdsChain {
     sel = (e & 0xffu) == b ? e : dead;
   }
   __device__ __forceinline__ bool dead_now() const { return sel == dead; }
-  // continue the walk over bytes [k, len) of the field at pos; rows with
-  // skip descriptors are handled at 8-byte block boundaries
+  // continue the walk over bytes [k, len) of the field at pos
   template <class Src>
   __device__ __forceinline__ void run(const uint32_t* __restrict__ img, const Src& src, uint32_t pos, uint32_t len,
                                       uint32_t k) {
 #define L7M_STEP(B) step(img, (B));
-    // 8-byte blocks (the dead state is absorbing: one exit test per block);
-    // a row with a skip descriptor is handled at the block boundary (slim =
-    // ~0u without descriptors: never)
-#ifdef L7M_SKIP
-    while (k + 8 <= len) {
-      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
-      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
-      const uint32_t b4 = src.byte(pos + k + 4), b5 = src.byte(pos + k + 5);
-      const uint32_t b6 = src.byte(pos + k + 6), b7 = src.byte(pos + k + 7);
-      L7M_STEP(b0)
-      L7M_STEP(b1)
-      L7M_STEP(b2)
-      L7M_STEP(b3)
-      L7M_STEP(b4)
-      L7M_STEP(b5)
-      L7M_STEP(b6)
-      L7M_STEP(b7)
-      k += 8;
-      if (dead_now()) return;
-#ifdef L7M_SKIP
-      // staged records (HBM-direct ones walk every byte: less code), and only
-      // with a long rest: a lane in the skip handler runs its own loop while
-      // the wave's other lanes wait, which costs more than walking a short
-      // rest in step with them (config 2's `/api/w/.*` tails: 3.56 -> 4.62 ms)
-      if constexpr (Src::kLds)
-        if ((sel >> kLdsRowShift) >= slim && len - k >= kSkipMinRest) k = skip(img, src, pos, len, k);
-#endif
-    }
-    if (k + 4 <= len && !dead_now()) {  // then at most one 4-byte block
-      const uint32_t b0 = src.byte(pos + k), b1 = src.byte(pos + k + 1);
-      const uint32_t b2 = src.byte(pos + k + 2), b3 = src.byte(pos + k + 3);
-      L7M_STEP(b0)
-      L7M_STEP(b1)
-      L7M_STEP(b2)
-      L7M_STEP(b3)
-      k += 4;
-    }
-    if (k < len && !dead_now()) {  // the last 1-3 bytes, no loop
-      L7M_STEP(src.byte(pos + k))
-      if (k + 1 < len) {
-        L7M_STEP(src.byte(pos + k + 1))
-        if (k + 2 < len) L7M_STEP(src.byte(pos + k + 2))
-      }
-    }
-#else
     L7M_WALK_BYTES(L7M_STEP, dead_now())
-#endif
 #undef L7M_STEP
   }
   __device__ __forceinline__ uint32_t code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
@@ -401,18 +304,6 @@ struct Codes<8> {
     const uint32_t lo = d & 2 ? b : a, hi = d & 2 ? f : e;
     return d & 4 ? hi : lo;
   }
-  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) {  // d wave-uniform
-    switch (d) {
-      case 0: r0 = v; break;
-      case 1: r1 = v; break;
-      case 2: r2 = v; break;
-      case 3: r3 = v; break;
-      case 4: r4 = v; break;
-      case 5: r5 = v; break;
-      case 6: r6 = v; break;
-      default: r7 = v; break;
-    }
-  }
 };
 template <>
 struct Codes<4> {  // programs with <= 4 value DFAs: four registers
@@ -428,14 +319,6 @@ struct Codes<4> {  // programs with <= 4 value DFAs: four registers
     const uint32_t a = d & 1 ? r1 : r0, b = d & 1 ? r3 : r2;
     return d & 2 ? b : a;
   }
-  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) {  // d wave-uniform
-    switch (d) {
-      case 0: r0 = v; break;
-      case 1: r1 = v; break;
-      case 2: r2 = v; break;
-      default: r3 = v; break;
-    }
-  }
 };
 template <>
 struct Codes<0> {
@@ -444,7 +327,6 @@ struct Codes<0> {
     for (uint32_t d = 0; d < n; ++d) p[d * kBlock] = 0;
   }
   __device__ __forceinline__ void set(uint32_t d, uint32_t v) { p[d * kBlock] = v; }
-  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) { p[d * kBlock] = v; }
   __device__ __forceinline__ uint32_t get(uint32_t d) const { return p[d * kBlock]; }
 };
 
@@ -462,7 +344,6 @@ struct Codes<-1> {
   __device__ __forceinline__ void set(uint32_t d, uint32_t v) {
     __hip_atomic_store(p + d * stride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __device__ __forceinline__ void set_u(uint32_t d, uint32_t v) { set(d, v); }
   __device__ __forceinline__ uint32_t get(uint32_t d) const {
     uint32_t v = __hip_atomic_load(p + d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" : "+v"(v));
@@ -475,8 +356,6 @@ struct Ctx {
   const uint32_t* img;         // LDS image
   const DfaDesc* dds;          // LDS
   const FieldDesc* fields;     // LDS
-  const DfaDesc* __restrict__ gdds;       // program copies (uniform reads: scalar loads)
-  const FieldDesc* __restrict__ gfields;
   const uint32_t* name_field;  // LDS
   const Span* sets;            // HBM
   const uint32_t* pool;        // HBM
@@ -501,14 +380,6 @@ __device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd,
     acc |= gld(mid + (e >> 24));
   }
   return acc | gld(c.prog + dd.es_off + st);
-}
-
-template <bool kLit, bool kSearch, class Src>
-__device__ __forceinline__ uint32_t walk_desc(const Ctx& c, const DfaDesc& dd, const Src& src, uint32_t pos,
-                                              uint32_t len) {
-  if (kSearch && dd.kind == kDfaSearch) return walk_search(c, dd, src, pos, len);
-  if (dd.lds_table != kNone) return walk_lds(c.img, c.prog, dd, src, pos, len);
-  return walk_hbm<kLit>(c.img, c.prog, dd, src, pos, len);
 }
 
 template <bool kLit, bool kSearch, class Src>
@@ -590,26 +461,18 @@ __device__ __forceinline__ uint32_t ent_lookup(const Ctx& c, const HttpHeader& h
   }
 }
 
-#ifdef L7M_PROF
-// Diagnostic build only: per-lane cycle accumulators per evaluation phase
-// (s_memtime), LDS-staged records only.  prof[0] = last timestamp.
-#define PROF_PARAM , uint64_t (&prof)[8]
-#define PROF_ARG , prof
-#define HPROF(i)                                      \
-  do {                                                \
-    if (Src::kLds) {                                  \
-      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-      prof[i] += t_ - prof[0];                        \
-      prof[0] = t_;                                   \
-    }                                                 \
-  } while (0)
-#else
-#define PROF_PARAM
-#define PROF_ARG
-#define HPROF(i) \
-  do {           \
-  } while (0)
-#endif
+// Diagnostic timeline (L7M_PROF builds, kProf): per-lane cycle accumulators
+// per evaluation phase (s_memtime), LDS-staged records only; prof[0] = last
+// timestamp.  Without kProf the accumulators are dead stores and vanish.
+template <bool kLds>
+__device__ __forceinline__ void hprof(uint64_t (&prof)[8], int i) {
+  if constexpr (kProf && kLds) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    prof[i] += t - prof[0];
+    prof[0] = t;
+  }
+}
+#define HPROF(i) hprof<Src::kLds>(prof, i)
 
 // What the walk phase of a record hands to its verification phase.
 template <int kReg>
@@ -619,10 +482,6 @@ struct WalkOut {
   uint32_t ex, e0;    // port entries whose rules may decide (exact port, port 0)
   uint32_t remote;    // the request's remote identity
   uint32_t pf_t;      // the candidate-entry touch (kept live until verification)
-#ifdef L7M_EPF
-  uint32_t pf_d;      // DFA whose candidate entry was touched, or kNone
-  uint32_t pf_ent;    // that entry's word offset in the program, or kNone
-#endif
   bool h0;            // the port-0 entry has HTTP rules
 };
 constexpr int32_t kNeedVerify = INT32_MIN;
@@ -634,10 +493,8 @@ constexpr int32_t kNeedVerify = INT32_MIN;
 // 1 = stop after the DFA walks, 2 = stop after record validation.
 template <int kReg, int kAblate, bool kLit, class Src>
 __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, const Src& src, uint64_t limit,
-                                             WalkOut<kReg>& o PROF_PARAM) {
-#ifdef L7M_PROF
-  if (Src::kLds) prof[0] = __builtin_amdgcn_s_memtime();
-#endif
+                                             WalkOut<kReg>& o, uint64_t (&prof)[8]) {
+  if constexpr (kProf && Src::kLds) prof[0] = __builtin_amdgcn_s_memtime();
   Codes<kReg>& codes = o.codes;
   if (limit < L7M_HTTP_REC_FIXED) return L7M_VERDICT_PARSE_ERROR;
   const uint32_t w0 = src.word(0), w1 = src.word(1), w2 = src.word(2), w3 = src.word(3), w4 = src.word(4);
@@ -697,68 +554,20 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
   // is touched (one dword load) as soon as that walk ends, so its L2 round
   // trip overlaps the remaining walks and verification reads the entry from
   // the CU's L1 (the walks in between touch no global memory).
-  uint32_t pf_d = kNone, pf_t = 0, pf_ent = kNone;
+  bool touched = false;
+  uint32_t pf_t = 0;
   auto touch = [&](uint32_t d, uint32_t code) {
-    if (pf_d == kNone && code && ((cand_all >> d) & 1ull)) {
+    if (!touched && code && ((cand_all >> d) & 1ull)) {
       const DfaDesc& dd = c.dds[d];
       if (dd.lds_ct == kNone && !(kReg < 0 && dd.kind == kDfaSearch)) {
         const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
-        pf_ent = dd.ct_off + 16u * idx;
-        pf_t = c.prog[pf_ent];
-        pf_d = d;
+        pf_t = c.prog[dd.ct_off + 16u * idx];
+        touched = true;
       }
     }
   };
   for (uint32_t job = 0;; ++job) {
     HPROF(4);  // (diagnostic build) what followed the previous job's walks
-#ifdef L7M_PAIR
-    // :path and :authority as two interleaved chains (h.pair_pa): their
-    // 8-byte blocks step together while both fields have one left, so each
-    // dependent LDS read overlaps the other chain's; the rests finish alone.
-    if (job == 1 && h.pair_pa) {
-      const uint32_t dP = c.fields[kFieldPath].dfa_first, dA = c.fields[kFieldAuthority].dfa_first;
-      const DfaDesc& ddP = c.dds[dP];
-      const DfaDesc& ddA = c.dds[dA];
-      const bool hasP = (flags & L7M_HTTP_F_PATH) != 0, hasA = (flags & L7M_HTTP_F_AUTHORITY) != 0;
-      const uint32_t posP = pos, posA = pos + plen;
-      const uint32_t lenP = ddP.start_base ? plen : 0u, lenA = ddA.start_base ? alen : 0u;
-      LdsChain cp, ca;
-      cp.init(ddP);
-      ca.init(ddA);
-      uint32_t kp = 0;
-      for (; kp + 4 <= lenP && kp + 4 <= lenA; kp += 4) {
-        const uint32_t p0 = src.byte(posP + kp), p1 = src.byte(posP + kp + 1), p2 = src.byte(posP + kp + 2),
-                       p3 = src.byte(posP + kp + 3);
-        const uint32_t a0 = src.byte(posA + kp), a1 = src.byte(posA + kp + 1), a2 = src.byte(posA + kp + 2),
-                       a3 = src.byte(posA + kp + 3);
-        cp.step(c.img, p0);
-        ca.step(c.img, a0);
-        cp.step(c.img, p1);
-        ca.step(c.img, a1);
-        cp.step(c.img, p2);
-        ca.step(c.img, a2);
-        cp.step(c.img, p3);
-        ca.step(c.img, a3);
-        if (cp.dead_now() && ca.dead_now()) {
-          kp += 4;
-          break;
-        }
-      }
-      if (lenP) cp.run(c.img, src, posP, lenP, kp < lenP ? kp : lenP);
-      if (lenA) ca.run(c.img, src, posA, lenA, kp < lenA ? kp : lenA);
-      const uint32_t codeP = hasP ? cp.code(c.img, c.prog, ddP) : 0u;
-      const uint32_t codeA = hasA ? ca.code(c.img, c.prog, ddA) : 0u;
-      if (hasP) present |= 1ull << kFieldPath;
-      if (hasA) present |= 1ull << kFieldAuthority;
-      codes.set(dP, codeP);
-      touch(dP, codeP);
-      codes.set(dA, codeA);
-      touch(dA, codeA);
-      pos += plen + alen;
-      ++job;  // the authority job is done
-      continue;
-    }
-#endif
     uint32_t f = kNone, p = pos, len = 0;
     if (job < 3) {
       len = job == 0 ? mlen : job == 1 ? plen : alen;
@@ -790,30 +599,6 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         ++hj;
       }
     }
-#ifdef L7M_UNIFORM
-    // The lanes' fields, one at a time (a waterfall; the pseudo-header jobs
-    // take one round): inside a round the field and its DFAs are
-    // wave-uniform, so their descriptors are scalar loads of the program's
-    // copies (SGPRs, no per-lane descriptor arithmetic) and the end code goes
-    // to its register by a uniform branch.
-    if (f != kNone) present |= 1ull << f;
-    bool todo = f != kNone;
-    for (;;) {
-      const uint64_t m = __ballot(todo);
-      if (!m) break;
-      const uint32_t fu = __builtin_amdgcn_readlane(f, static_cast<uint32_t>(__builtin_ctzll(m)));
-      if (todo && f == fu) {
-        todo = false;
-        const FieldDesc& fd = c.gfields[fu];
-        for (uint32_t k = 0; k < fd.ndfa; ++k) {
-          const uint32_t d = fd.dfa_first + k;
-          const uint32_t code = walk_desc<kLit, (kReg < 0)>(c, c.gdds[d], src, p, len);
-          codes.set_u(d, code);
-          touch(d, code);
-        }
-      }
-    }
-#else
     HPROF(2);  // job selection, header-name lookup
     if (f != kNone) {
       present |= 1ull << f;
@@ -826,7 +611,6 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         touch(d, code);
       }
     }
-#endif
   }
 
   HPROF(5);
@@ -841,31 +625,17 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
   o.h0 = h0;
   o.remote = w1;
   o.pf_t = pf_t;
-#ifdef L7M_EPF
-  o.pf_d = pf_d;
-  o.pf_ent = pf_ent;
-#else
-  (void)pf_d;
-  (void)pf_ent;
-#endif
   return kNeedVerify;
 }
 
 // Verification phase: the first rule (smallest index) among the keyed
 // candidates whose other matchers, port entry and remote set hold; the
 // check-record lists are selected by the walks' end codes.
-// `pe` holds the first 48 bytes of the candidate entry the walk phase touched
-// (o.pf_d), loaded before the next tile's bytes were requested: vmcnt counts
-// loads in issue order, so an entry load issued here would wait for them.
 template <int kReg>
-__device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o,
-                                               const u32x4 (&pe)[3]) {
+__device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o) {
   const Codes<kReg>& codes = o.codes;
   const uint64_t present = o.present;
-#ifndef L7M_EPF
-  (void)pe;
   asm volatile("" ::"v"(o.pf_t));  // the touch completes here, not at its first use
-#endif
   const uint32_t ex = o.ex, e0 = o.e0, remote = o.remote;
   const bool h0 = o.h0;
   // a rule may decide only if it belongs to ex, or to e0 when e0 has HTTP rules
@@ -922,10 +692,7 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
       if (rid >= best) return;
       const uint32_t ma[4] = {q1.x, q1.z, q2.x, q2.z}, mp[4] = {q1.y, q1.w, q2.y, q2.w};
       bool ok = eligible(hd) && (!(hd & kCrRemote) || remote_ok(rid));
-#ifndef L7M_VSERIAL
-      if constexpr (kReg < 0)
-#endif
-      {  // search programs (mask codes): one matcher after the other
+      if constexpr (kReg < 0) {  // search programs (mask codes): one matcher after the other
 #pragma unroll
         for (uint32_t q = 0; q < kCandInlineMatchers; ++q) {
           if (q < nm && ok) {
@@ -934,14 +701,11 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
             else if (!((a >> 8) & 1u)) ok = code_has<(kReg < 0)>(c, a >> 9, codes.get(a >> 9), mp[q]);
           }
         }
-      }
-#ifndef L7M_VSERIAL
-      else
-      // The inline matchers in two rounds of independent LDS reads (each
-      // DFA's mask table, then the set's mask word) instead of one dependent
-      // chain per matcher; set codes whose masks are not in LDS (or search
-      // automata) take the general code_has.
-      {
+      } else {
+        // The inline matchers in two rounds of independent LDS reads (each
+        // DFA's mask table, then the set's mask word) instead of one dependent
+        // chain per matcher; set codes whose masks are not in LDS take the
+        // general code_has.
         uint32_t cq[4], mo[4], w[4];
         bool need[4], set[4];
 #pragma unroll
@@ -976,7 +740,6 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
           }
         }
       }
-#endif
       if (ok) best = rid;
     } else {
       scan(Span{q0.y, len});
@@ -1021,11 +784,7 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
     if (!((mw >> (idx & 31u)) & 1u)) continue;  // no candidates
     if (dd.lds_ct != kNone) {
       check_inline(c.img + dd.lds_ct + 16u * idx);
-#ifdef L7M_EPF
-    } else if (d == o.pf_d) {
-      check_entry(pe[0], pe[1], pe[2]);
-#endif
-    } else {  // an HBM candidate entry (L7M_EPF: one that was not prefetched)
+    } else {  // an HBM candidate entry (touched by the walk phase)
       typedef __attribute__((address_space(1))) const u32x4* gq;
       const gq q = (gq)(c.prog + dd.ct_off + 16u * idx);
       u32x4 q0 = q[0], q1 = q[1], q2 = q[2];
@@ -1091,9 +850,7 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
   const uint32_t n_ctr = h.n_rules + 2;
   uint32_t* ctr = smem + h.lds_image_words;  // LDS hit counters (kLdsHits)
   uint32_t* col = ctr + (kHits == kLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);  // LDS code columns (!kReg)
-  // pfz: the workgroup's 256-byte sink of the L2 prefetch (never read)
-  uint8_t* pfz = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock));
-  uint8_t* stg = pfz + kPrefetchSink + wv * (stage + 16u);
+  uint8_t* stg = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock)) + wv * (stage + 16u);
   {
     const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
     uint4* l = reinterpret_cast<uint4*>(img);
@@ -1108,41 +865,26 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
   c.img = img;
   c.dds = reinterpret_cast<const DfaDesc*>(img + h.lds_dfas);
   c.fields = reinterpret_cast<const FieldDesc*>(img + h.lds_fields);
-  c.gdds = reinterpret_cast<const DfaDesc*>(prog + h.off_dfas);
-  c.gfields = reinterpret_cast<const FieldDesc*>(prog + h.off_fields);
   c.name_field = img + h.lds_name_field;
   c.sets = reinterpret_cast<const Span*>(prog + h.off_sets);
   c.pool = prog + h.off_pool;
   c.cr = prog + h.off_cr;
   c.remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
   uint32_t* mycol = col + tid;
-#ifdef L7M_PROF
+  // diagnostic wave timeline per tile (kProf, s_memtime): [0] top wait,
+  // [1] walks, [2] entry wait, [3] issue, [4] verify + store, [5] counters;
+  // [6] tiles
   uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t prof_tile = 0;
-  // wave timeline per tile (s_memtime): [0] top wait, [1] walks, [2] entry
-  // wait, [3] issue, [4] verify + store, [5] counters; [6] tiles
-  uint64_t qt[7] = {0, 0, 0, 0, 0, 0, 0}, qlast = __builtin_amdgcn_s_memtime();
-#define QT(i)                                              \
-  do {                                                     \
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
-    qt[i] += t_ - qlast;                                   \
-    qlast = t_;                                            \
-  } while (0)
-#define QTN(i)                                             \
-  do {                                                     \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
-    qt[i] += t_ - qlast;                                   \
-    qlast = t_;                                            \
-  } while (0)
-#else
-#define QT(i) \
-  do {        \
-  } while (0)
-#define QTN(i) QT(i)
-#endif
+  uint64_t prof_tile = 0, te0 = 0;
+  uint64_t qt[7] = {0, 0, 0, 0, 0, 0, 0}, qlast = kProf ? __builtin_amdgcn_s_memtime() : 0;
+  auto qtn = [&](int i) {
+    if constexpr (kProf) {
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      qt[i] += t_ - qlast;
+      qlast = t_;
+    }
+  };
 
   // This wave's contiguous share of the batch, consumed in tiles of <= 64
   // records.  Software pipeline per wave: while tile t is evaluated from the
@@ -1184,42 +926,23 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     t.take = t.k ? t.k : 1u;
     return t;
   };
-  // Staging.  LDS-DMA staging (the default: global_load_lds_dwordx4,
-  // non-temporal): the next tile's bytes go HBM -> the wave's stage with no
-  // VGPR destination and no ds_write pass (lane l of piece `it` lands at
-  // stage + it * 1 KiB + 16 l, the coalesced copy's own layout), issued after
-  // the walks, the stage's only readers.  Register staging (L7M_REGSTAGE,
-  // except for the literal-table instantiation, whose register-staged build
-  // spills): the bytes are loaded into VGPRs after the walks and written to
-  // the stage at the top of the next iteration.  Measured on the round-3
-  // kernel: LDS-DMA 3.47-3.49 vs 3.52 ms on config 2, 8.83 vs 8.93 on
-  // config 4 (128 -> 105 VGPRs); the early round-3 kernel measured the
-  // opposite (3.58 vs 3.51).
-#ifdef L7M_REGSTAGE
-  constexpr bool kDma = kLit;
-#else
-  constexpr bool kDma = true;
-#endif
-  u32x4 buf[kCopyIters];
+  // Staging by LDS-DMA (global_load_lds_dwordx4, non-temporal): the next
+  // tile's bytes go HBM -> the wave's stage with no VGPR destination and no
+  // ds_write pass (lane l of piece `it` lands at stage + it * 1 KiB + 16 l,
+  // the coalesced copy's own layout), issued after the walks, the stage's
+  // only readers.  (Register staging measured 3.52 vs 3.47-3.49 ms on config
+  // 2, 8.93 vs 8.83 on config 4: profiles/r03/ab_round3.md.)
   auto issue_bytes = [&](const Tile& t) {
     const u32x4* src = reinterpret_cast<const u32x4*>(arena + t.base);
-    if constexpr (kDma) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's stage reads are done
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this tile's stage reads are done
 #pragma unroll
-      for (uint32_t it = 0; it < kCopyIters; ++it) {
-        const uint32_t q = it * 64u + lane;
-        if (q * 16u < t.bytes)
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
-                                           reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                               reinterpret_cast<uintptr_t>(stg + it * 1024u)),
-                                           16, 0, 2);
-      }
-    } else {
-#pragma unroll
-      for (uint32_t it = 0; it < kCopyIters; ++it) {
-        const uint32_t q = it * 64u + lane;
-        if (q * 16u < t.bytes) buf[it] = __builtin_nontemporal_load(src + q);
-      }
+    for (uint32_t it = 0; it < kCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < t.bytes)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(stg + it * 1024u)),
+                                         16, 0, 2);
     }
   };
   uint64_t o1, n1, o2, n2;
@@ -1228,38 +951,14 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
   issue_bytes(t);
   load_offs(t.cur + t.take, &o2, &n2);
   while (t.cur < end) {
-    if constexpr (kDma) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
-    } else {
-#pragma unroll
-      for (uint32_t it = 0; it < kCopyIters; ++it) {
-        const uint32_t q = it * 64u + lane;
-        if (q * 16u < t.bytes) reinterpret_cast<u32x4*>(stg)[q] = buf[it];
-      }
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed
     wave_sync();
-    QTN(0);
-#ifdef L7M_L2PF
-    // The next tile's window is pulled into L2 now, while this tile is
-    // walked (one 4-byte LDS-DMA per 128-byte line, into the sink), so its
-    // LDS-DMA copy after the walks waits for L2 instead of HBM: a wave holds
-    // one stage, so the copy itself cannot be issued before the walks.
-    {
-      const Tile tp = plan(t.cur + t.take, o2, n2);
-      if (lane * 128u < tp.bytes)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(arena + tp.base + lane * 128u),
-                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                             reinterpret_cast<uintptr_t>(pfz)),
-                                         4, 0, 0);
-    }
-#endif
+    qtn(0);
 
     const uint64_t o = t.o, onext = t.onext, base = t.base;
     const uint32_t k = t.k, take = t.take;
     int32_t v = 0;
-#ifdef L7M_PROF
-    const uint64_t te0 = __builtin_amdgcn_s_memtime();
-#endif
+    if constexpr (kProf) te0 = __builtin_amdgcn_s_memtime();
     WalkOut<kReg> wo;
     if constexpr (!kReg) wo.codes.p = mycol;
     if constexpr (kReg < 0) {  // search programs: the codes live in the global scratch
@@ -1272,48 +971,31 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
         const LdsSrc s{reinterpret_cast<const uint32_t*>(stg + (o - base))};
         const uint32_t w0 = s.word(0);
         if (((static_cast<uint64_t>(w0) + 3) & ~3ull) <= onext - o) {
-          v = eval_walk<kReg, kAblate, kLit>(c, h, s, onext - o, wo PROF_ARG);
+          v = eval_walk<kReg, kAblate, kLit>(c, h, s, onext - o, wo, prof);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: read HBM directly
         const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
         const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-        v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo PROF_ARG) : L7M_VERDICT_PARSE_ERROR;
+        v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo, prof) : L7M_VERDICT_PARSE_ERROR;
       }
     }
-    QTN(1);
-    u32x4 pe[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-#ifdef L7M_EPF
-    // (experiment, measured 1 % slower on config 2) the touched candidate
-    // entry is loaded and waited for BEFORE the next tile's bytes are
-    // requested: vmcnt is in-order, so verification reading it later waits
-    // for those bytes too
-    if (lane < take && v == kNeedVerify && wo.pf_ent != kNone) {
-      asm volatile("" ::"v"(wo.pf_t));  // the touch completes here, not at its first use
-      const u32x4* e = reinterpret_cast<const u32x4*>(c.prog + wo.pf_ent);
-      pe[0] = e[0];
-      pe[1] = e[1];
-      pe[2] = e[2];
-    }
-    asm volatile("" : "+v"(pe[0]), "+v"(pe[1]), "+v"(pe[2]));  // landed here
-#endif
-    QTN(2);
+    qtn(1);
+    qtn(2);
     // The next tile's bytes are requested only now, after the walks: they
     // land during verification without holding kCopyIters x 4 registers
     // through the walks (the walks read LDS only).
     const Tile t2 = plan(t.cur + t.take, o2, n2);
     issue_bytes(t2);
     load_offs(t2.cur + t2.take, &o2, &n2);
-    QTN(3);
+    qtn(3);
     if (lane < take) {
-      if (v == kNeedVerify) v = eval_verify<kReg>(c, h, wo, pe);
+      if (v == kNeedVerify) v = eval_verify<kReg>(c, h, wo);
       verdicts[t.cur + lane] = v;
     }
-    QTN(4);
-#ifdef L7M_PROF
-    prof_tile += __builtin_amdgcn_s_memtime() - te0;
-#endif
+    qtn(4);
+    if constexpr (kProf) prof_tile += __builtin_amdgcn_s_memtime() - te0;
     if (kHits != kNoHits) {
       uint32_t slot = kNone;
       // allows decided without a rule (no L7 rules, no port policy) are not counted
@@ -1331,13 +1013,10 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     }
     wave_sync();  // the stage is overwritten by the next tile
     t = t2;
-    QTN(5);
-#ifdef L7M_PROF
+    qtn(5);
     qt[6] += 1;
-#endif
   }
-#ifdef L7M_PROF
-  if ((blockIdx.x == 0 && wv == 0) || (blockIdx.x == 101 && wv == 7)) {
+  if (kProf && ((blockIdx.x == 0 && wv == 0) || (blockIdx.x == 101 && wv == 7))) {
     if (lane == 0)
       printf("L7M_QT block %u wave %u tiles %llu cycles/tile: topwait %llu walks %llu entry %llu issue %llu "
              "verify %llu counters %llu\n",
@@ -1357,7 +1036,6 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
              (unsigned long long)prof[4], (unsigned long long)prof[5], (unsigned long long)prof[6],
              (unsigned long long)prof[7]);
   }
-#endif
   if (kHits == kLdsHits) {
     __syncthreads();
     for (uint32_t i = tid; i < n_ctr; i += kBlock)
@@ -1371,7 +1049,7 @@ size_t http_lds_bytes(const HttpHeader& h, uint32_t stage) {
   const bool reg = h.n_dfas <= kRegDfas || h.search;  // search programs: codes in global scratch
   const size_t ctr = h.n_rules + 2 <= kMaxLdsCounters ? ((h.n_rules + 2 + 3) & ~size_t(3)) : 0;
   return 4u * (static_cast<size_t>(h.lds_image_words) + ctr + (reg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock)) +
-         kPrefetchSink + static_cast<size_t>(kWaves) * (stage + 16u);
+         static_cast<size_t>(kWaves) * (stage + 16u);
 }
 
 // Bytes of records staged per wave: what is left of the LDS after the tables.

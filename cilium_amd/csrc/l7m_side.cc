@@ -585,7 +585,7 @@ void l7m_proxy_stats_table_destroy(l7m_proxy_stats_table* t) { delete t; }
 int l7m_proxy_stats_update(l7m_proxy_stats_table* t, uint32_t proto, const uint8_t* arena, size_t arena_bytes,
                            const uint64_t* offs, const int32_t* verdicts, size_t n, uint16_t port, int ingress) {
   if (!t || (n && !verdicts) || (proto != L7M_PROTO_HTTP && proto != L7M_PROTO_KAFKA)) return L7M_EINVAL;
-  if (proto == L7M_PROTO_HTTP && n && (!arena || !offs)) return L7M_EINVAL;
+  if (n && (!arena || !offs)) return L7M_EINVAL;
   std::lock_guard<std::mutex> g(t->mu);
   for (size_t i = 0; i < n; ++i) {
     const int32_t vd = verdicts[i];
@@ -605,10 +605,20 @@ int l7m_proxy_stats_update(l7m_proxy_stats_table* t, uint32_t proto, const uint8
       // request ReadRequest rejected (the connection closes) (kafka.go:213-229,349-354)
       if (vd == L7M_VERDICT_PARSE_ERROR) continue;
     }
+    uint32_t fv = flow_verdict(vd);
+    if (proto == L7M_PROTO_KAFKA && vd == L7M_VERDICT_DENY) {
+      // a denied request is answered with CreateResponse(ErrTopicAuthorizationFailed),
+      // which fails for the kinds ReadRequest leaves untyped (request == nil,
+      // request.go:174-175): the record is then logged as VerdictError
+      // (kafka.go:246-252)
+      size_t len = 0;
+      KReq q;
+      if (kafka_rec(arena, arena_bytes, offs[i], &len) && read_kafka(arena + offs[i], len, &q) == L7M_EUNSUPPORTED)
+        fv = 2;
+    }
     if (p == 0 && proto == L7M_PROTO_KAFKA) continue;
     l7m_proxy_stats& s = t->m[std::make_tuple(proto, p, ing, 1u)];
     s.received++;
-    const uint32_t fv = flow_verdict(vd);
     if (fv == 0) s.forwarded++;
     else if (fv == 1) s.denied++;
     else s.error++;

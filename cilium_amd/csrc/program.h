@@ -143,16 +143,6 @@ constexpr uint32_t kMaxLdsCounters = 8192;       // per-rule hit counters kept i
 constexpr uint32_t kHttpMinStage = 2048;         // smallest record stage per wave (bytes)
 constexpr uint32_t kHttpMaxStage = 8192;         // largest record stage per wave (bytes)
 constexpr uint32_t kMaxLdsCtmaskWords = 256;     // candidate-presence bitmask kept in LDS up to this
-#ifdef L7M_L2PF
-constexpr uint32_t kHttpPrefetchSink = 256;      // LDS bytes the next tile's L2 prefetch writes (64 lanes x 4)
-#else
-constexpr uint32_t kHttpPrefetchSink = 0;
-#endif
-#ifdef L7M_SKIP
-constexpr bool kSkipRowsInKernel = true;         // the HTTP kernel follows skip descriptors (dfa_pack.h)
-#else
-constexpr bool kSkipRowsInKernel = false;
-#endif
 
 struct FieldDesc {
   uint32_t dfa_first, ndfa;  // value DFAs of this field (contiguous)

@@ -414,7 +414,10 @@ int l7m_proxy_stats_add(const int32_t* verdicts, size_t n, l7m_proxy_stats* stat
  *           is not counted, nor a request ReadRequest rejected (the proxy
  *           closes the connection) (pkg/proxy/kafka.go:213-229, 349-354).
  * Verdicts: allowed -> forwarded, L7M_VERDICT_DENY -> denied, others ->
- * error.  Thread-safe.  l7m_proxy_stats_get copies up to cap entries in key
+ * error; a denied Kafka request of a kind ReadRequest leaves untyped counts
+ * as error (its deny response cannot be built, pkg/proxy/kafka.go:246-252,
+ * pkg/kafka/request.go:174-175).  The records are read for both protocols
+ * (arena / rec_offsets required).  Thread-safe.  l7m_proxy_stats_get copies up to cap entries in key
  * order and returns the number of entries. */
 typedef struct l7m_proxy_stats_table l7m_proxy_stats_table;
 typedef struct {
@@ -486,7 +489,9 @@ size_t l7m_kafka_api_key_name(int16_t api_key, char* out, size_t cap);
  * [arena, arena + arena_bytes + 64) lies inside one such allocation (16-byte
  * aligned) runs the kernels on it in place over PCIe, with no staging copy
  * (zero-copy; L7M_ZERO_COPY=0 in the environment disables it); other arenas
- * are copied.  l7m_host_mapped(p, bytes) = 1 when [p, p + bytes) qualifies. */
+ * are copied.  The 64 bytes past arena_bytes are readable slack only: the
+ * kernels may read them but never use their contents as record data (the
+ * copying path zero-fills them, the zero-copy path leaves them as they are).  l7m_host_mapped(p, bytes) = 1 when [p, p + bytes) qualifies. */
 int l7m_alloc_pinned(size_t bytes, void** out);
 void l7m_free_pinned(void* p);
 int l7m_host_mapped(const void* p, size_t bytes);

@@ -28,6 +28,7 @@
 #include <bitset>
 #include <cstdint>
 #include <stdexcept>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -52,6 +53,11 @@ struct Inst {
 struct Prog {
   std::vector<Inst> code;  // entry at 0; kByte / kSet / assertions fall through to pc + 1
   std::vector<ByteSet> sets;
+  // Bytes every full match must start with (forced_prefix): a necessary
+  // condition checked before the simulation, so a linear scan over many rules
+  // rejects most of them with one compare.
+  std::string prefix;
+  bool exact = false;  // the pattern's language is {prefix} (a literal)
 };
 
 namespace detail {
@@ -499,6 +505,44 @@ inline Prog compile(const std::string& pattern) {
   detail::Compiler cc(ps.nodes, &p);
   cc.emit(root);
   p.code.push_back(Inst{kMatch, 0, 0, 0});
+  // Forced prefix: from the current point, the epsilon closure taken with
+  // every assertion passing (a superset of the real closure) holds exactly one
+  // consuming instruction, a single byte, and no match: that byte must come
+  // next.  Sound for full match, whatever the assertions decide.
+  std::vector<uint32_t> stack, seen(p.code.size(), 0);
+  uint32_t gen = 0, pc0 = 0;
+  bool asserts = false;
+  while (p.prefix.size() < 256) {
+    ++gen;
+    stack.assign(1, pc0);
+    int consumers = 0;
+    uint32_t only = 0;
+    bool match = false;
+    while (!stack.empty()) {
+      const uint32_t pc = stack.back();
+      stack.pop_back();
+      if (seen[pc] == gen) continue;
+      seen[pc] = gen;
+      const Inst& in = p.code[pc];
+      switch (in.op) {
+        case kByte: case kSet: ++consumers; only = pc; break;
+        case kMatch: match = true; break;
+        case kJmp: stack.push_back(in.x); break;
+        case kSplit: stack.push_back(in.y); stack.push_back(in.x); break;
+        default: asserts = true; stack.push_back(pc + 1); break;  // assertions: assumed to pass
+      }
+    }
+    if (match && consumers == 0 && !asserts) p.exact = true;
+    if (match || consumers != 1) break;
+    const Inst& in = p.code[only];
+    int ch = in.op == kByte ? in.ch : -1;
+    if (in.op == kSet && p.sets[in.x].count() == 1)
+      for (int c = 0; c < 256; ++c)
+        if (p.sets[in.x].test(c)) ch = c;
+    if (ch < 0) break;
+    p.prefix.push_back(static_cast<char>(ch));
+    pc0 = only + 1;
+  }
   return p;
 }
 
@@ -506,6 +550,8 @@ inline Prog compile(const std::string& pattern) {
 class Runner {
  public:
   bool run(const Prog& p, const uint8_t* s, size_t n, bool search) {
+    if (!search && (n < p.prefix.size() || std::memcmp(s, p.prefix.data(), p.prefix.size()) != 0)) return false;
+    if (!search && p.exact) return n == p.prefix.size();
     const size_t m = p.code.size();
     if (sparse_.size() < m) {
       sparse_.assign(m, 0);

@@ -189,3 +189,17 @@ def test_proxy_stats_keyed_like_the_endpoint():
     assert e == {("http", 80, True, True): {"received": 2, "forwarded": 1, "denied": 1, "error": 0},
                  ("http", 8080, False, True): {"received": 1, "forwarded": 1, "denied": 0, "error": 0},
                  ("kafka", 9092, True, True): {"received": 3, "forwarded": 1, "denied": 1, "error": 1}}
+
+
+def test_proxy_stats_denied_untyped_kafka_kind_is_error():
+    """A denied request of a kind ReadRequest leaves untyped (heartbeat = 12,
+    request == nil) cannot get its deny response: CreateResponse fails
+    (pkg/kafka/request.go:174-175) and handleRequest logs VerdictError
+    (pkg/proxy/kafka.go:246-252), so the endpoint counts an error; an allowed
+    one is forwarded, a denied typed one is denied."""
+    t = L.ProxyStatsTable()
+    recs = [K.generic(12, 0, "c"), K.generic(12, 0, "c"), K.metadata(0, "c", ["x"])]
+    arena, offs = L.pack_records(recs)
+    t.update(L.PROTO_KAFKA, arena, offs, np.array([L.VERDICT_DENY, 0, L.VERDICT_DENY], np.int32), port=9092,
+             ingress=False)
+    assert t.entries() == {("kafka", 9092, False, True): {"received": 3, "forwarded": 1, "denied": 1, "error": 1}}

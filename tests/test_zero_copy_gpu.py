@@ -28,10 +28,18 @@ class Pinned:
 
 
 def _pinned_copy(arena, shift=0, slack=256):
+    """The arena in pinned memory; the bytes around it (the 64-byte pad past
+    arena_bytes included) are 0xff: the pad's contents must not matter."""
     pb = Pinned(arena.nbytes + shift + slack)
-    pb.a[:] = 0
+    pb.a[:] = 0xFF
     pb.a[shift:shift + arena.nbytes] = arena
     return pb, pb.a[shift:shift + arena.nbytes]
+
+
+def _mapped(view):
+    """Would l7m_eval read this arena in place? (l7m_api.cc: 16-byte aligned,
+    and the padded range (arena_bytes + 64) & ~3 inside one pinned allocation)"""
+    return bool(view.ctypes.data % 16 == 0 and L._lib.l7m_host_mapped(view.ctypes.data, (view.nbytes + 64) & ~3))
 
 
 def _pinned_u64(x):
@@ -50,6 +58,8 @@ def test_http_zero_copy_matches_copying_path(gpu):
     pa, view = _pinned_copy(arena)
     po, poffs = _pinned_u64(offs)
     try:
+        assert _mapped(view), "the pinned arena must take the zero-copy path"
+        assert L._lib.l7m_host_mapped(poffs.ctypes.data, poffs.nbytes) == 1
         for o in (offs, poffs):  # offsets copied, then read in place too
             hits = np.zeros_like(hits_ref)
             got = rs.eval(view, o, hits)
@@ -68,8 +78,16 @@ def test_http_zero_copy_falls_back_on_misaligned_or_short_ranges(gpu):
     arena, offs = W.requests(2, 0, 20_000, n_rules=100)
     ref = rs.eval(arena.copy(), offs)
     pa, view = _pinned_copy(arena, shift=4)  # arena pointer 4 mod 16: copying path
-    pb, view2 = _pinned_copy(arena, slack=0)  # padded range past the allocation: copying path
+    # padded range past the allocation: an allocation of whole pages holding
+    # the arena at its end, so the 64-byte pad cannot fit, whatever the
+    # allocator rounds to
+    size = (arena.nbytes + 15 + 4095) // 4096 * 4096
+    pb = Pinned(size)
+    at = (size - arena.nbytes) & ~15
+    pb.a[at:at + arena.nbytes] = arena
+    view2 = pb.a[at:at + arena.nbytes]
     try:
+        assert not _mapped(view) and not _mapped(view2)
         assert np.array_equal(rs.eval(view, offs), ref)
         assert np.array_equal(rs.eval(view2, offs), ref)
     finally:
@@ -86,6 +104,7 @@ def test_kafka_zero_copy_with_compressed_sets(gpu):
     ref = rs.eval(arena.copy(), offs)
     pa, view = _pinned_copy(arena)
     try:
+        assert _mapped(view)
         assert np.array_equal(rs.eval(view, offs), ref)
     finally:
         pa.free()
