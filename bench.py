@@ -101,7 +101,9 @@ def cpu_baseline(cfg, rules, seconds, threads):
     from oracle import HttpOracle, KafkaOracle  # test infrastructure: cpu_baseline leg only
     proto = W.CONFIGS[cfg]["proto"]
     engine = "nfa" if cfg == 5 else "std"
-    orc = HttpOracle(rules, engine=engine) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+    # the reference's per-request loop as Envoy runs it: every rule's matchers,
+    # no prefilter (parity_leg uses the prefiltered scan)
+    orc = HttpOracle(rules, engine=engine, prefilter=False) if proto == L.PROTO_HTTP else KafkaOracle(rules)
     n0 = 20_000 if cfg != 5 else 16 * threads
 
     def sample(start, n):
@@ -512,7 +514,8 @@ def run_mixed(args, world, rank, dev, scaling):
         from oracle import HttpOracle, KafkaOracle  # test infrastructure: cpu_baseline leg only
         n_tot, t_tot, samples = 0, 0.0, []
         for p in parts:
-            orc = HttpOracle(p["rules"]) if p["proto"] == L.PROTO_HTTP else KafkaOracle(p["rules"])
+            orc = (HttpOracle(p["rules"], prefilter=False) if p["proto"] == L.PROTO_HTTP
+                   else KafkaOracle(p["rules"]))
             a, o = W.requests(p["gcfg"], 10_000_000, 5_000, seed=p["seed"], n_rules=len(p["rules"]),
                               threads=threads)
             t1 = time.perf_counter()

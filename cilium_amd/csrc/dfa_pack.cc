@@ -43,9 +43,12 @@ void flatten_cat(const re::Ast& a, int node, std::vector<int>* seq) {
   }
 }
 
+// Assertions whose answer depends on where the residual starts: '^' (only at
+// position 0) and '\b' / '\B' (the byte before); look-ahead is kept out of
+// residuals too (its automaton is built with the residual's own start).
 bool has_bol(const re::Ast& a, int node) {
   const re::Node& n = a.nodes[node];
-  if (n.kind == re::Node::Bol) return true;
+  if (n.kind == re::Node::Bol || n.kind == re::Node::WordB || n.kind == re::Node::Look) return true;
   for (int k : n.kids)
     if (has_bol(a, k)) return true;
   return false;
@@ -88,8 +91,9 @@ int copy_node(const re::Ast& src, int node, re::Ast* dst, std::string* key) {
     case re::Node::Cat:
     case re::Node::Alt:
     case re::Node::Rep:
-      key->push_back(n.kind == re::Node::Cat ? 'C' : n.kind == re::Node::Alt ? 'A' : 'R');
-      if (n.kind == re::Node::Rep) {
+    case re::Node::Look:
+      key->push_back(n.kind == re::Node::Cat ? 'C' : n.kind == re::Node::Alt ? 'A' : n.kind == re::Node::Rep ? 'R' : 'L');
+      if (n.kind == re::Node::Rep || n.kind == re::Node::Look) {
         put32(key, static_cast<uint32_t>(n.min));
         put32(key, static_cast<uint32_t>(n.max));
       }
@@ -99,6 +103,11 @@ int copy_node(const re::Ast& src, int node, re::Ast* dst, std::string* key) {
     case re::Node::Bol: key->push_back('^'); break;
     case re::Node::Eol: key->push_back('$'); break;
     case re::Node::Empty: key->push_back('e'); break;
+    case re::Node::WordB: key->push_back(n.min ? 'B' : 'b'); break;
+    case re::Node::Group:
+    case re::Node::Backref:  // (removed by lower_for_dfa before any automaton is built)
+      key->push_back('?');
+      break;
   }
   dst->nodes.push_back(std::move(m));
   return static_cast<int>(dst->nodes.size()) - 1;

@@ -36,6 +36,10 @@ namespace {
 
 std::string cstr(const char* p) { return p ? std::string(p) : std::string(); }
 
+// States of one look-ahead pattern's exact automaton before it is carried as
+// a superset (the look-ahead dropped) and decided by the slow path.
+constexpr size_t kLookMaxStates = 1u << 16;
+
 // Go strings.SplitN(s, " ", 2)
 std::vector<std::string> split2(const std::string& s) {
   size_t k = s.find(' ');
@@ -348,12 +352,28 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
                                             ": " + e.what() + " (Envoy would NACK the policy)");
         }
         std::string perr;
-        re::Status st = re::parse_ecma(fp.value, &asts[p], &perr);
+        re::Ast full;
+        re::Status st = re::parse_ecma(fp.value, &full, &perr);
         if (st == re::Status::TooBig)
           return fail(L7M_ETOOBIG, "regex '" + fp.value + "': " + perr);
         if (st != re::Status::Ok)
-          return fail(L7M_EUNSUPPORTED, "regex '" + fp.value + "': " + perr +
-                                            " is outside the compiled (regular) subset");
+          return fail(L7M_EUNSUPPORTED, "regex '" + fp.value + "': " + perr + " (parser disagrees with std::regex)");
+        bool exact = true;
+        asts[p] = re::lower_for_dfa(full, &exact);
+        if (exact && re::has_node(asts[p], re::Node::Look)) {
+          // look-ahead is determinised exactly (regex_ecma.cc build_ctx)
+          // unless its automaton exceeds kLookMaxStates: then the DFA carries
+          // the pattern without it (a superset) and the slow path decides
+          re::Dfa probe;
+          re::DfaLimits ll;
+          ll.max_states = kLookMaxStates;
+          if (re::build_dfa({&asts[p]}, ll, &probe) != re::Status::Ok) {
+            asts[p] = re::drop_lookahead(asts[p]);
+            exact = false;
+          }
+        }
+        if (!exact)
+          return fail(L7M_EUNSUPPORTED, "regex '" + fp.value + "': back-reference (slow path not built)");
       } else {
         asts[p] = re::literal_ast(fp.value);
       }

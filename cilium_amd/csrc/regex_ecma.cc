@@ -23,6 +23,7 @@
 #include <locale>
 #include <map>
 #include <unordered_map>
+#include <unordered_set>
 
 namespace l7m {
 namespace re {
@@ -129,6 +130,7 @@ class Parser {
       val_ = static_cast<unsigned char>(*hit);
     } else if (c == 'b' || c == 'B') {
       tok_ = T_WORDB;
+      val_ = c;
     } else if (c == 'd' || c == 'D' || c == 's' || c == 'S' || c == 'w' || c == 'W') {
       tok_ = T_QCLASS;
       val_ = c;
@@ -148,8 +150,14 @@ class Parser {
       tok_ = T_HEX;
       val_ = v & 0xff;  // _M_value.assign(1, int) narrows to char
     } else if (is_digit(c)) {
-      while (!at_end() && is_digit(cur())) ++i_;
+      unsigned long long v = c - '0';
+      while (!at_end() && is_digit(cur())) {
+        v = v * 10 + (cur() - '0');
+        if (v > (1ull << 30)) v = 1ull << 30;
+        ++i_;
+      }
       tok_ = T_BACKREF;
+      num_ = v;
     } else {
       tok_ = T_ORD;
       val_ = c;
@@ -230,7 +238,10 @@ class Parser {
           if (at_end()) fail(Status::Syntax, "(? at end");
           unsigned char d = p_[i_++];
           if (d == ':') tok_ = T_SUBNG;
-          else if (d == '=' || d == '!') tok_ = T_LOOKAHEAD;
+          else if (d == '=' || d == '!') {
+            tok_ = T_LOOKAHEAD;
+            val_ = d;
+          }
           else fail(Status::Syntax, "bad (?");
         } else {
           tok_ = T_SUB;
@@ -302,11 +313,29 @@ class Parser {
     return add(std::move(n));
   }
 
+  // _M_term: an assertion (^ $ \b \B (?=X) (?!X)) takes no quantifier.
   int term() {
     if (tok_ == T_BOL) { advance(); return mk(Node::Bol); }
     if (tok_ == T_EOL) { advance(); return mk(Node::Eol); }
-    if (tok_ == T_WORDB) fail(Status::Unsupported, "\\b / \\B word boundary");
-    if (tok_ == T_LOOKAHEAD) fail(Status::Unsupported, "look-ahead");
+    if (tok_ == T_WORDB) {
+      const bool neg = val_ == 'B';
+      advance();
+      Node n;
+      n.kind = Node::WordB;
+      n.min = neg ? 1 : 0;
+      return add(std::move(n));
+    }
+    if (tok_ == T_LOOKAHEAD) {
+      const bool neg = val_ == '!';
+      advance();
+      const int r = disjunction();
+      if (!match(T_SUBEND)) fail(Status::Syntax, "missing )");
+      Node n;
+      n.kind = Node::Look;
+      n.min = neg ? 1 : 0;
+      n.kids = {r};
+      return add(std::move(n));
+    }
     int a = atom();
     if (a < 0) return -1;
     for (;;) {
@@ -317,19 +346,20 @@ class Parser {
     return a;
   }
 
-  int rep(int kid, int mn, int mx) {
+  int rep(int kid, int mn, int mx, bool lazy) {
     Node n;
     n.kind = Node::Rep;
     n.kids = {kid};
     n.min = mn;
     n.max = mx;
+    n.lazy = lazy;
     return add(std::move(n));
   }
 
   int quantifier(int a) {
-    if (match(T_STAR)) { match(T_OPT); return rep(a, 0, -1); }
-    if (match(T_PLUS)) { match(T_OPT); return rep(a, 1, -1); }
-    if (match(T_OPT)) { match(T_OPT); return rep(a, 0, 1); }
+    if (match(T_STAR)) return rep(a, 0, -1, match(T_OPT));
+    if (match(T_PLUS)) return rep(a, 1, -1, match(T_OPT));
+    if (match(T_OPT)) return rep(a, 0, 1, match(T_OPT));
     if (match(T_IBEGIN)) {
       if (tok_ != T_DUP) fail(Status::Syntax, "bad brace");
       unsigned long long mn = num_;
@@ -344,10 +374,10 @@ class Parser {
         }
       }
       if (!match(T_IEND)) fail(Status::Syntax, "bad brace");
-      match(T_OPT);
+      const bool lazy = match(T_OPT);
       if (mx >= 0 && mx < static_cast<long long>(mn)) fail(Status::Syntax, "bad brace range");
       if (mn > 100000 || mx > 100000) fail(Status::TooBig, "repeat count");
-      return rep(a, static_cast<int>(mn), static_cast<int>(mx));
+      return rep(a, static_cast<int>(mn), static_cast<int>(mx), lazy);
     }
     return -1;
   }
@@ -369,7 +399,15 @@ class Parser {
       s.set(v);
       return mk_set(s);
     }
-    if (tok_ == T_BACKREF) fail(Status::Unsupported, "back-reference");
+    if (tok_ == T_BACKREF) {
+      const unsigned long long k = num_;
+      advance();
+      if (k < 1 || k >= static_cast<unsigned long long>(groups_)) fail(Status::Syntax, "back-reference");
+      Node n;
+      n.kind = Node::Backref;
+      n.min = static_cast<int>(k);
+      return add(std::move(n));
+    }
     if (tok_ == T_QCLASS) {
       unsigned char c = static_cast<unsigned char>(val_);
       advance();
@@ -378,11 +416,22 @@ class Parser {
       if (c >= 'A' && c <= 'Z') s.flip();
       return mk_set(s);
     }
-    if (tok_ == T_SUBNG || tok_ == T_SUB) {
+    if (tok_ == T_SUBNG) {
       advance();
       int r = disjunction();
       if (!match(T_SUBEND)) fail(Status::Syntax, "missing )");
       return r;
+    }
+    if (tok_ == T_SUB) {  // capture group: numbered by its '(' (_M_insert_subexpr_begin)
+      advance();
+      const int idx = groups_++;
+      int r = disjunction();
+      if (!match(T_SUBEND)) fail(Status::Syntax, "missing )");
+      Node n;
+      n.kind = Node::Group;
+      n.min = idx;
+      n.kids = {r};
+      return add(std::move(n));
     }
     if (tok_ == T_BRACK || tok_ == T_BRACKNEG) {
       bool neg = tok_ == T_BRACKNEG;
@@ -507,20 +556,37 @@ class Parser {
   unsigned long long num_ = 0;
   std::string str_;
   Ast ast_;
+  int groups_ = 1;  // capture groups opened so far + 1 (group 0 = the whole match)
 };
 
 // ------------------------------------------------------------------- NFA --
 struct NState {
-  enum : uint8_t { CHR, SPLIT, EPS, BOL, EOL, MATCH } type;
+  enum : uint8_t { CHR, SPLIT, EPS, BOL, EOL, MATCH, WORDB, LOOK } type;
   int out1 = -1, out2 = -1;
-  int cs = -1;   // CHR: set id
-  int pat = -1;  // MATCH: pattern id
+  int cs = -1;   // CHR: set id; LOOK: look-ahead automaton id
+  int pat = -1;  // MATCH: pattern id; WORDB / LOOK: 1 = negated
+};
+
+// The automaton of a look-ahead (?=X) / (?!X): the DFA of X [\x00-\xff]*
+// read as a full match of the rest of the subject -- libstdc++'s sub-executor
+// (regex_executor.tcc _M_lookahead) runs X in prefix mode on [current, end)
+// with current as its own begin, so '^' inside X holds at the look-ahead's
+// position and '\b' there sees no character before it, exactly as for a
+// subject that starts there.  `universal` marks the states from which every
+// continuation is accepted at the end (the obligation is met, whatever follows).
+struct LookDfa {
+  Dfa dfa;
+  std::vector<uint8_t> universal;
+  bool neg = false;
 };
 
 struct Nfa {
   std::vector<NState> st;
   std::vector<ByteSet> sets;
   std::unordered_map<std::string, int> set_ids;
+  std::vector<LookDfa> looks;
+  bool ctx = false;  // has WORDB / LOOK states (context construction)
+  DfaLimits lim;
   size_t limit = 8u << 20;
 
   int add(NState s) {
@@ -537,6 +603,8 @@ struct Nfa {
     set_ids.emplace(std::move(key), id);
     return id;
   }
+
+  int look_dfa(const Ast& a, int node, bool neg);
 
   // Thompson construction: returns the entry state of `node` continuing to `next`.
   int compile(const Ast& a, int node, int next) {
@@ -558,6 +626,27 @@ struct Nfa {
         s.out1 = next;
         return add(s);
       }
+      case Node::WordB: {
+        NState s;
+        s.type = NState::WORDB;
+        s.pat = n.min;
+        s.out1 = next;
+        ctx = true;
+        return add(s);
+      }
+      case Node::Look: {
+        NState s;
+        s.type = NState::LOOK;
+        s.pat = n.min;
+        s.cs = look_dfa(a, n.kids[0], n.min != 0);
+        s.out1 = next;
+        ctx = true;
+        return add(s);
+      }
+      case Node::Group:
+        return compile(a, n.kids[0], next);
+      case Node::Backref:
+        throw ParseError{Status::Unsupported, "back-reference (lower_for_dfa first)"};
       case Node::Cat: {
         int cur = next;
         for (size_t k = n.kids.size(); k-- > 0;) cur = compile(a, n.kids[k], cur);
@@ -659,6 +748,8 @@ class Closure {
           if (eol) stack_.push_back(x.out1);
           else out->push_back(s);
           break;
+        default:  // WORDB / LOOK: build_ctx's closure
+          break;
       }
     }
     std::sort(out->begin(), out->end());
@@ -718,8 +809,446 @@ void make_search_prefix(Ast* a) {
   a->root = static_cast<int>(a->nodes.size()) - 1;
 }
 
+namespace {
+
+// Moore minimisation (initial partition by end set and mid set) and BFS
+// renumbering of an unminimised DFA (n0 states x ncls classes, state 0 dead).
+Status finish_dfa(size_t n0, int ncls, const int* cls, const std::vector<uint32_t>& next,
+                  const std::vector<uint32_t>& endset, const std::vector<uint32_t>& midset, int start_id,
+                  std::vector<std::vector<uint32_t>>&& sets, const DfaLimits& lim, bool with_mid, Dfa* out) {
+  // Moore minimisation: initial partition by end set (and mid set).
+  std::vector<uint32_t> blk(n0);
+  size_t nblk = 0;
+  {
+    // dense renumber
+    std::unordered_map<uint64_t, uint32_t> rn;
+    for (size_t s = 0; s < n0; ++s) {
+      const uint64_t key = static_cast<uint64_t>(midset[s]) << 32 | endset[s];
+      auto it = rn.find(key);
+      if (it == rn.end()) it = rn.emplace(key, static_cast<uint32_t>(rn.size())).first;
+      blk[s] = it->second;
+    }
+    nblk = rn.size();
+  }
+  std::vector<uint32_t> sig(static_cast<size_t>(ncls) + 1);
+  for (;;) {
+    std::unordered_map<std::vector<uint32_t>, uint32_t, U32VecHash> sigs;
+    sigs.reserve(nblk * 2 + 16);
+    std::vector<uint32_t> nb(n0);
+    for (size_t s = 0; s < n0; ++s) {
+      sig[0] = blk[s];
+      for (int c = 0; c < ncls; ++c) sig[c + 1] = blk[next[s * ncls + c]];
+      auto it = sigs.find(sig);
+      if (it == sigs.end()) it = sigs.emplace(sig, static_cast<uint32_t>(sigs.size())).first;
+      nb[s] = it->second;
+    }
+    size_t nn = sigs.size();
+    blk.swap(nb);
+    if (nn == nblk) break;
+    nblk = nn;
+  }
+
+  // BFS renumbering over blocks; dead block -> 0.
+  std::vector<int64_t> newid(nblk, -1);
+  std::vector<size_t> rep(nblk, SIZE_MAX);
+  for (size_t s = 0; s < n0; ++s)
+    if (rep[blk[s]] == SIZE_MAX) rep[blk[s]] = s;
+  newid[blk[0]] = 0;
+  std::vector<uint32_t> order;  // block ids in new-id order
+  order.push_back(blk[0]);
+  size_t head = 0;
+  if (newid[blk[start_id]] < 0) {
+    newid[blk[start_id]] = static_cast<int64_t>(order.size());
+    order.push_back(blk[start_id]);
+  }
+  head = 1;
+  while (head < order.size()) {
+    uint32_t b = order[head++];
+    size_t s = rep[b];
+    for (int c = 0; c < ncls; ++c) {
+      uint32_t tb = blk[next[s * ncls + c]];
+      if (newid[tb] < 0) {
+        newid[tb] = static_cast<int64_t>(order.size());
+        order.push_back(tb);
+      }
+    }
+  }
+  const size_t nst = order.size();
+  if (nst > lim.max_states) return Status::TooBig;
+  if (static_cast<uint64_t>(nst) * (ncls + 1) * 4 > lim.max_table_bytes) return Status::TooBig;
+
+  Dfa d;
+  d.ncls = ncls;
+  for (int b = 0; b < 256; ++b) d.cmap[b] = static_cast<uint8_t>(cls[b]);
+  d.nstates = static_cast<int>(nst);
+  d.start = static_cast<int>(newid[blk[start_id]]);
+  d.next.assign(nst * ncls, 0);
+  d.endset.assign(nst, 0);
+  if (with_mid) d.midset.assign(nst, 0);
+  for (size_t i = 0; i < nst; ++i) {
+    size_t s = rep[order[i]];
+    for (int c = 0; c < ncls; ++c)
+      d.next[i * ncls + c] = static_cast<uint32_t>(newid[blk[next[s * ncls + c]]]);
+    d.endset[i] = endset[s];
+    if (with_mid) d.midset[i] = midset[s];
+  }
+  d.sets = std::move(sets);
+  *out = std::move(d);
+  return Status::Ok;
+}
+
+}  // namespace
+
+namespace {
+
+ByteSet word_set() { return mask_set(std::ctype_base::alnum, true); }  // _M_is_word: lookup_classname("w")
+
+int copy_subtree(const Ast& a, int node, Ast* dst) {
+  Node m = a.nodes[node];
+  for (int& k : m.kids) k = copy_subtree(a, k, dst);
+  dst->nodes.push_back(std::move(m));
+  return static_cast<int>(dst->nodes.size()) - 1;
+}
+
+// ---------------------------------------------- context construction ----
+// Patterns with word boundaries or look-ahead.  A DFA state is a set of
+// threads (NFA state + look-ahead obligations) plus the context the pending
+// assertions need: whether this is the subject's start ('^') and whether the
+// previous byte was a word character ('\b').  Assertions are resolved with
+// the byte being consumed as their right context (or the end of the subject);
+// a look-ahead at position i starts an obligation: its automaton (LookDfa)
+// runs from i and must accept at the end of the subject ((?=X)) or must not
+// ((?!X)); obligations whose automaton reaches the dead state or a universal
+// state are decided early.
+using Th = std::vector<int>;  // [nfa state, look id, look state, look id, look state, ...] (sorted pairs)
+
+struct CtxIn {
+  bool bol, eol, prev;
+  int next;  // -1 unknown (assertions needing it stay pending), 0 non-word / end, 1 word
+};
+
+void th_add_obl(Th* t, int la, int q) {
+  for (size_t k = 1; k < t->size(); k += 2)
+    if ((*t)[k] == la && (*t)[k + 1] == q) return;
+  t->push_back(la);
+  t->push_back(q);
+  std::vector<std::pair<int, int>> o;
+  for (size_t k = 1; k < t->size(); k += 2) o.push_back({(*t)[k], (*t)[k + 1]});
+  std::sort(o.begin(), o.end());
+  for (size_t k = 0; k < o.size(); ++k) {
+    (*t)[1 + 2 * k] = o[k].first;
+    (*t)[2 + 2 * k] = o[k].second;
+  }
+}
+
+struct ThHash {
+  size_t operator()(const Th& v) const {
+    uint64_t h = 1469598103934665603ull;
+    for (int x : v) {
+      h ^= static_cast<uint32_t>(x);
+      h *= 1099511628211ull;
+    }
+    return static_cast<size_t>(h ^ (h >> 29));
+  }
+};
+
+class CtxClosure {
+ public:
+  explicit CtxClosure(const Nfa& n) : n_(n) {}
+  void run(const std::vector<Th>& seeds, const CtxIn& c, std::vector<Th>* out) {
+    out->clear();
+    seen_.clear();
+    stack_ = seeds;
+    while (!stack_.empty()) {
+      Th t = std::move(stack_.back());
+      stack_.pop_back();
+      if (!seen_.insert(t).second) continue;
+      const NState& x = n_.st[t[0]];
+      auto go = [&](int to) {
+        Th u = t;
+        u[0] = to;
+        stack_.push_back(std::move(u));
+      };
+      switch (x.type) {
+        case NState::CHR:
+        case NState::MATCH:
+          out->push_back(t);
+          break;
+        case NState::SPLIT:
+          go(x.out2);
+          go(x.out1);
+          break;
+        case NState::EPS:
+          go(x.out1);
+          break;
+        case NState::BOL:
+          if (c.bol) go(x.out1);
+          break;
+        case NState::EOL:
+          if (c.eol) go(x.out1);
+          else out->push_back(t);
+          break;
+        case NState::WORDB:
+          if (c.next < 0) out->push_back(t);
+          else if ((c.prev != (c.next == 1)) == (x.pat == 0)) go(x.out1);
+          break;
+        case NState::LOOK: {
+          const LookDfa& l = n_.looks[x.cs];
+          const uint32_t q = static_cast<uint32_t>(l.dfa.start);
+          if (c.eol) {
+            if ((l.dfa.endset[q] != 0) != l.neg) go(x.out1);
+          } else if (q == 0) {
+            if (l.neg) go(x.out1);
+          } else if (l.universal[q]) {
+            if (!l.neg) go(x.out1);
+          } else {
+            Th u = t;
+            u[0] = x.out1;
+            th_add_obl(&u, x.cs, static_cast<int>(q));
+            stack_.push_back(std::move(u));
+          }
+          break;
+        }
+      }
+    }
+    std::sort(out->begin(), out->end());
+    out->erase(std::unique(out->begin(), out->end()), out->end());
+  }
+  // Consume byte b in every obligation of t; false if the thread dies.
+  bool advance(Th* t, int b) const {
+    Th u{(*t)[0]};
+    for (size_t k = 1; k < t->size(); k += 2) {
+      const LookDfa& l = n_.looks[(*t)[k]];
+      const uint32_t q = l.dfa.next[static_cast<size_t>((*t)[k + 1]) * l.dfa.ncls + l.dfa.cmap[b]];
+      if (q == 0) {
+        if (!l.neg) return false;
+        continue;  // (?!X): X can no longer match
+      }
+      if (l.universal[q]) {
+        if (l.neg) return false;
+        continue;  // (?=X): X has matched
+      }
+      th_add_obl(&u, (*t)[k], static_cast<int>(q));
+    }
+    *t = std::move(u);
+    return true;
+  }
+  // At the end of the subject: do t's obligations hold?
+  bool obligations_hold(const Th& t) const {
+    for (size_t k = 1; k < t.size(); k += 2) {
+      const LookDfa& l = n_.looks[t[k]];
+      if ((l.dfa.endset[t[k + 1]] != 0) == l.neg) return false;
+    }
+    return true;
+  }
+
+ private:
+  const Nfa& n_;
+  std::unordered_set<Th, ThHash> seen_;
+  std::vector<Th> stack_;
+};
+
+Status build_ctx(const Nfa& nfa, const std::vector<int>& starts, int ncls, const int* cls, const DfaLimits& lim,
+                 Dfa* out) {
+  std::vector<int> rep(ncls, -1);
+  for (int b = 0; b < 256; ++b)
+    if (rep[cls[b]] < 0) rep[cls[b]] = b;
+  const ByteSet W = word_set();
+  bool any_wb = false;
+  for (const NState& x : nfa.st) any_wb |= x.type == NState::WORDB;
+  struct St {
+    std::vector<Th> th;
+    bool start, prev;
+  };
+  std::vector<St> states(1);  // 0 = dead
+  std::unordered_map<Th, int, ThHash> ids;
+  std::vector<uint32_t> next(static_cast<size_t>(ncls), 0);
+  auto intern = [&](std::vector<Th>&& th, bool start, bool prev) -> int {
+    if (th.empty()) return 0;
+    Th key{(start ? 1 : 0) | (prev ? 2 : 0)};
+    for (const Th& t : th) {
+      key.push_back(static_cast<int>(t.size()));
+      key.insert(key.end(), t.begin(), t.end());
+    }
+    auto it = ids.find(key);
+    if (it != ids.end()) return it->second;
+    const int id = static_cast<int>(states.size());
+    if (static_cast<size_t>(id) >= lim.max_states) throw ParseError{Status::TooBig, "context DFA too large"};
+    ids.emplace(std::move(key), id);
+    states.push_back(St{std::move(th), start, prev});
+    next.resize(next.size() + ncls, 0);
+    return id;
+  };
+  CtxClosure clo(nfa);
+  std::vector<Th> seeds, k1, k2;
+  int start_id;
+  try {
+    for (int s0 : starts) seeds.push_back(Th{s0});
+    clo.run(seeds, CtxIn{true, false, false, -1}, &k1);
+    start_id = intern(std::move(k1), true, false);
+    for (size_t d = 1; d < states.size(); ++d) {
+      for (int c = 0; c < ncls; ++c) {
+        const int b = rep[c];
+        const bool bw = W.test(b);
+        clo.run(states[d].th, CtxIn{states[d].start, false, states[d].prev, bw ? 1 : 0}, &k1);
+        seeds.clear();
+        for (const Th& t : k1) {
+          const NState& x = nfa.st[t[0]];
+          if (x.type != NState::CHR || !nfa.sets[x.cs].test(b)) continue;
+          Th u = t;
+          u[0] = x.out1;
+          if (clo.advance(&u, b)) seeds.push_back(std::move(u));
+        }
+        clo.run(seeds, CtxIn{false, false, bw, -1}, &k2);
+        const int to = intern(std::move(k2), false, any_wb && bw);
+        next[d * ncls + c] = static_cast<uint32_t>(to);
+      }
+    }
+  } catch (const ParseError& e) {
+    return e.st;
+  }
+  if (start_id == 0) {  // nothing can match: a one-state dead automaton with a start row
+    start_id = static_cast<int>(states.size());
+    states.push_back(St{{}, true, false});
+    next.resize(next.size() + ncls, 0);
+  }
+  const size_t n0 = states.size();
+  std::vector<std::vector<uint32_t>> sets{{}};
+  std::unordered_map<std::vector<uint32_t>, uint32_t, U32VecHash> set_ids{{std::vector<uint32_t>{}, 0}};
+  std::vector<uint32_t> endset(n0, 0), midset(n0, 0);
+  for (size_t d = 1; d < n0; ++d) {
+    clo.run(states[d].th, CtxIn{states[d].start, true, states[d].prev, 0}, &k1);
+    std::vector<uint32_t> pats;
+    for (const Th& t : k1)
+      if (nfa.st[t[0]].type == NState::MATCH && clo.obligations_hold(t))
+        pats.push_back(static_cast<uint32_t>(nfa.st[t[0]].pat));
+    std::sort(pats.begin(), pats.end());
+    pats.erase(std::unique(pats.begin(), pats.end()), pats.end());
+    auto it = set_ids.find(pats);
+    if (it == set_ids.end()) {
+      it = set_ids.emplace(pats, static_cast<uint32_t>(sets.size())).first;
+      sets.push_back(pats);
+    }
+    endset[d] = it->second;
+  }
+  states.clear();
+  return finish_dfa(n0, ncls, cls, next, endset, midset, start_id, std::move(sets), lim, false, out);
+}
+
+}  // namespace
+
+int Nfa::look_dfa(const Ast& a, int node, bool neg) {
+  // X [\x00-\xff]*, determinised as a subject of its own (see LookDfa)
+  Ast x;
+  const int xr = copy_subtree(a, node, &x);
+  Node any;
+  any.kind = Node::Set;
+  any.set.set();
+  x.nodes.push_back(any);
+  Node star;
+  star.kind = Node::Rep;
+  star.min = 0;
+  star.max = -1;
+  star.kids = {static_cast<int>(x.nodes.size()) - 1};
+  x.nodes.push_back(star);
+  Node cat;
+  cat.kind = Node::Cat;
+  cat.kids = {xr, static_cast<int>(x.nodes.size()) - 1};
+  x.nodes.push_back(cat);
+  x.root = static_cast<int>(x.nodes.size()) - 1;
+  LookDfa l;
+  l.neg = neg;
+  const Status st = build_dfa({&x}, lim, &l.dfa);
+  if (st != Status::Ok) throw ParseError{st, "look-ahead automaton"};
+  const Dfa& d = l.dfa;
+  l.universal.assign(d.nstates, 0);
+  for (int q = 0; q < d.nstates; ++q) l.universal[q] = d.endset[q] != 0;
+  for (bool changed = true; changed;) {
+    changed = false;
+    for (int q = 0; q < d.nstates; ++q) {
+      if (!l.universal[q]) continue;
+      for (int c = 0; c < d.ncls; ++c)
+        if (!l.universal[d.next[static_cast<size_t>(q) * d.ncls + c]]) {
+          l.universal[q] = 0;
+          changed = true;
+          break;
+        }
+    }
+  }
+  looks.push_back(std::move(l));
+  return static_cast<int>(looks.size()) - 1;
+}
+
+bool has_node(const Ast& a, Node::Kind k) {
+  for (const Node& n : a.nodes)
+    if (n.kind == k) return true;
+  return false;
+}
+
+namespace {
+// in_ref: copying a group's pattern for a back-reference -- the reference
+// compares text only, so the group's assertions (checked where the group
+// matched) do not apply at the reference's position and are dropped.
+int lower_node(const Ast& a, int node, Ast* dst, const std::vector<int>& gnode, bool* exact, bool drop_look,
+               bool in_ref = false) {
+  const Node& n = a.nodes[node];
+  auto empty = [&]() {
+    Node e;
+    e.kind = Node::Empty;
+    dst->nodes.push_back(e);
+    return static_cast<int>(dst->nodes.size()) - 1;
+  };
+  switch (n.kind) {
+    case Node::Group:
+      return lower_node(a, n.kids[0], dst, gnode, exact, drop_look, in_ref);
+    case Node::Backref:
+      // \k matches the text group k captured: a string of group k's language
+      *exact = false;
+      return lower_node(a, a.nodes[gnode[n.min]].kids[0], dst, gnode, exact, drop_look, true);
+    case Node::Look:
+      if (drop_look || in_ref) {
+        *exact = false;
+        return empty();
+      }
+      break;
+    case Node::WordB:
+    case Node::Bol:
+    case Node::Eol:
+      if (in_ref) return empty();
+      break;
+    default:
+      break;
+  }
+  Node m = n;
+  for (int& k : m.kids) k = lower_node(a, k, dst, gnode, exact, drop_look, in_ref);
+  dst->nodes.push_back(std::move(m));
+  return static_cast<int>(dst->nodes.size()) - 1;
+}
+
+Ast lower(const Ast& a, bool* exact, bool drop_look) {
+  std::vector<int> gnode;
+  for (size_t i = 0; i < a.nodes.size(); ++i)
+    if (a.nodes[i].kind == Node::Group) {
+      if (gnode.size() <= static_cast<size_t>(a.nodes[i].min)) gnode.resize(a.nodes[i].min + 1, -1);
+      gnode[a.nodes[i].min] = static_cast<int>(i);
+    }
+  Ast out;
+  *exact = true;
+  out.root = lower_node(a, a.root, &out, gnode, exact, drop_look);
+  return out;
+}
+}  // namespace
+
+Ast lower_for_dfa(const Ast& a, bool* exact) { return lower(a, exact, false); }
+
+Ast drop_lookahead(const Ast& a) {
+  bool exact;
+  return lower(a, &exact, true);
+}
+
 Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, Dfa* out, bool with_mid) {
   Nfa nfa;
+  nfa.lim = lim;
   std::vector<int> starts;
   try {
     for (size_t p = 0; p < patterns.size(); ++p) {
@@ -733,10 +1262,22 @@ Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, 
     return e.st;
   }
 
-  // Byte classes: refine the partition of 0..255 by every CHR set.
+  // Byte classes: refine the partition of 0..255 by every CHR set (and, for
+  // the context construction, by \w and every look-ahead automaton's classes).
+  std::vector<ByteSet> parts = nfa.sets;
+  if (nfa.ctx) {
+    parts.push_back(word_set());
+    for (const LookDfa& l : nfa.looks)
+      for (int c = 0; c < l.dfa.ncls; ++c) {
+        ByteSet b;
+        for (int x = 0; x < 256; ++x)
+          if (l.dfa.cmap[x] == c) b.set(x);
+        parts.push_back(b);
+      }
+  }
   int cls[256] = {0};
   int ncls = 1;
-  for (const ByteSet& s : nfa.sets) {
+  for (const ByteSet& s : parts) {
     std::map<std::pair<int, int>, int> remap;
     int n2 = 0;
     int tmp[256];
@@ -758,6 +1299,10 @@ Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, 
       if (rn[cls[b]] < 0) rn[cls[b]] = k++;
     for (int b = 0; b < 256; ++b) cls[b] = rn[cls[b]];
     ncls = k;
+  }
+  if (nfa.ctx) {
+    if (with_mid) return Status::Unsupported;  // (search automata carry no assertions)
+    return build_ctx(nfa, starts, ncls, cls, lim, out);
   }
   std::vector<std::vector<int>> set_classes(nfa.sets.size());
   for (size_t i = 0; i < nfa.sets.size(); ++i) {
@@ -855,86 +1400,7 @@ Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, 
   }
   kern.clear();
   kern.shrink_to_fit();
-
-  // Moore minimisation: initial partition by end set (and mid set).
-  std::vector<uint32_t> blk(n0);
-  size_t nblk = 0;
-  {
-    // dense renumber
-    std::unordered_map<uint64_t, uint32_t> rn;
-    for (size_t s = 0; s < n0; ++s) {
-      const uint64_t key = static_cast<uint64_t>(midset[s]) << 32 | endset[s];
-      auto it = rn.find(key);
-      if (it == rn.end()) it = rn.emplace(key, static_cast<uint32_t>(rn.size())).first;
-      blk[s] = it->second;
-    }
-    nblk = rn.size();
-  }
-  std::vector<uint32_t> sig(static_cast<size_t>(ncls) + 1);
-  for (;;) {
-    std::unordered_map<std::vector<uint32_t>, uint32_t, U32VecHash> sigs;
-    sigs.reserve(nblk * 2 + 16);
-    std::vector<uint32_t> nb(n0);
-    for (size_t s = 0; s < n0; ++s) {
-      sig[0] = blk[s];
-      for (int c = 0; c < ncls; ++c) sig[c + 1] = blk[next[s * ncls + c]];
-      auto it = sigs.find(sig);
-      if (it == sigs.end()) it = sigs.emplace(sig, static_cast<uint32_t>(sigs.size())).first;
-      nb[s] = it->second;
-    }
-    size_t nn = sigs.size();
-    blk.swap(nb);
-    if (nn == nblk) break;
-    nblk = nn;
-  }
-
-  // BFS renumbering over blocks; dead block -> 0.
-  std::vector<int64_t> newid(nblk, -1);
-  std::vector<size_t> rep(nblk, SIZE_MAX);
-  for (size_t s = 0; s < n0; ++s)
-    if (rep[blk[s]] == SIZE_MAX) rep[blk[s]] = s;
-  newid[blk[0]] = 0;
-  std::vector<uint32_t> order;  // block ids in new-id order
-  order.push_back(blk[0]);
-  size_t head = 0;
-  if (newid[blk[start_id]] < 0) {
-    newid[blk[start_id]] = static_cast<int64_t>(order.size());
-    order.push_back(blk[start_id]);
-  }
-  head = 1;
-  while (head < order.size()) {
-    uint32_t b = order[head++];
-    size_t s = rep[b];
-    for (int c = 0; c < ncls; ++c) {
-      uint32_t tb = blk[next[s * ncls + c]];
-      if (newid[tb] < 0) {
-        newid[tb] = static_cast<int64_t>(order.size());
-        order.push_back(tb);
-      }
-    }
-  }
-  const size_t nst = order.size();
-  if (nst > lim.max_states) return Status::TooBig;
-  if (static_cast<uint64_t>(nst) * (ncls + 1) * 4 > lim.max_table_bytes) return Status::TooBig;
-
-  Dfa d;
-  d.ncls = ncls;
-  for (int b = 0; b < 256; ++b) d.cmap[b] = static_cast<uint8_t>(cls[b]);
-  d.nstates = static_cast<int>(nst);
-  d.start = static_cast<int>(newid[blk[start_id]]);
-  d.next.assign(nst * ncls, 0);
-  d.endset.assign(nst, 0);
-  if (with_mid) d.midset.assign(nst, 0);
-  for (size_t i = 0; i < nst; ++i) {
-    size_t s = rep[order[i]];
-    for (int c = 0; c < ncls; ++c)
-      d.next[i * ncls + c] = static_cast<uint32_t>(newid[blk[next[s * ncls + c]]]);
-    d.endset[i] = endset[s];
-    if (with_mid) d.midset[i] = midset[s];
-  }
-  d.sets = std::move(sets);
-  *out = std::move(d);
-  return Status::Ok;
+  return finish_dfa(n0, ncls, cls, next, endset, midset, start_id, std::move(sets), lim, with_mid, out);
 }
 
 }  // namespace re

@@ -9,8 +9,12 @@
 // ECMAScript grammar (scanner/compiler of GCC 11) as an AST, lowers it to a
 // Thompson NFA and determinises a *set* of patterns into one DFA whose end
 // column reports which patterns matched.  No backtracking, no recursion on the
-// input: membership is exact for the regular subset (everything except
-// back-references, look-ahead and \b / \B, which are reported Unsupported).
+// input.  Word boundaries (\b / \B) and look-ahead ((?=X) / (?!X)) are
+// regular and determinised exactly (build_dfa's context / obligation
+// construction); back-references are not regular: lower_for_dfa replaces them
+// (and any look-ahead past the DFA limits) by a superset and marks the
+// pattern for the exact slow path (regex_vm.h), which restates libstdc++'s
+// backtracking executor.
 #pragma once
 #include <bitset>
 #include <cstdint>
@@ -25,10 +29,15 @@ using ByteSet = std::bitset<256>;
 enum class Status { Ok = 0, Syntax = 1, Unsupported = 2, TooBig = 3 };
 
 struct Node {
-  enum Kind : uint8_t { Empty, Set, Cat, Alt, Rep, Bol, Eol } kind = Empty;
+  // Group / Backref appear only in parse_ecma's full AST (lower_for_dfa
+  // removes them); WordB / Look are determinised by build_dfa.
+  enum Kind : uint8_t { Empty, Set, Cat, Alt, Rep, Bol, Eol, WordB, Look, Group, Backref } kind = Empty;
   ByteSet set;            // Set
-  std::vector<int> kids;  // Cat / Alt / Rep(1)
-  int min = 0, max = 0;   // Rep; max < 0 = unbounded
+  std::vector<int> kids;  // Cat / Alt / Rep(1) / Look(1: the looked-ahead pattern) / Group(1)
+  int min = 0, max = 0;   // Rep: repeat bounds, max < 0 = unbounded
+                          // WordB / Look: min = 1 for the negated form (\B, (?!X))
+                          // Group / Backref: min = capture index (1-based)
+  bool lazy = false;      // Rep: non-greedy ('?' after the quantifier; exploration order only)
 };
 
 struct Ast {
@@ -36,11 +45,23 @@ struct Ast {
   int root = -1;
 };
 
-// Parse `pat` with the libstdc++ ECMAScript grammar.  Patterns that
+// Parse `pat` with the libstdc++ ECMAScript grammar into the full AST (capture
+// groups, back-references, word boundaries, look-ahead).  Patterns that
 // std::regex rejects are expected to be filtered by the caller first (the
 // compiler validates with std::regex itself); this parser reports Syntax for
-// anything it cannot parse and Unsupported for non-regular constructs.
+// anything it cannot parse.
 Status parse_ecma(const std::string& pat, Ast* out, std::string* err);
+
+// The AST build_dfa determinises: capture groups dissolved, every
+// back-reference \k replaced by a copy of group k's pattern (a superset: the
+// referenced text is a string that group matched).  *exact = false when a
+// back-reference was replaced (the DFA's answer is then a superset and the
+// pattern needs the slow path).
+Ast lower_for_dfa(const Ast& a, bool* exact);
+// Look-ahead replaced by the empty pattern (a superset), for patterns whose
+// exact automaton exceeds the limits.
+Ast drop_lookahead(const Ast& a);
+bool has_node(const Ast& a, Node::Kind k);
 
 // Parse `pat` as Go regexp (RE2) syntax for L7M_DIALECT_RE2_SEARCH
 // (regex_re2.cc): Syntax where regexp.Compile fails, Unsupported for valid

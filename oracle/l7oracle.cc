@@ -109,6 +109,7 @@ struct HttpOracle {
   std::vector<std::unordered_set<uint32_t>> remotes;  // allowed_remotes_ (empty = any)
   std::unordered_map<std::string, uint32_t> name_ids;  // lower-cased header names of the rules
   std::vector<RulePre> pre;
+  bool prefilter = true;  // orc_http_set_prefilter(h, 0): the plain scan (bench.py's cpu_baseline)
 };
 
 bool hm_less(const Matcher& a, const Matcher& b) {
@@ -182,7 +183,7 @@ int32_t eval_http_one(const HttpOracle& o, const HttpReq& q) {
   for (size_t i = 0; i < o.rules.size(); ++i) {
     const RulePre& pr = o.pre[i];
     bool cand = true;
-    for (uint32_t k = 0; k < pr.n && cand; ++k) {
+    for (uint32_t k = 0; o.prefilter && k < pr.n && cand; ++k) {
       const std::string* v = vals[pr.nid[k]];
       cand = v && v->size() >= pr.len[k] && std::memcmp(v->data(), pr.b[k], pr.len[k]) == 0;
     }
@@ -1087,6 +1088,10 @@ int orc_http_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint6
 }
 
 void orc_http_free(void* h) { delete static_cast<HttpOracle*>(h); }
+
+// 0: evaluate every rule's matchers (the reference's per-request loop as
+// Envoy runs it), 1 (default): skip rules the per-rule prefilter rejects.
+void orc_http_set_prefilter(void* h, int on) { static_cast<HttpOracle*>(h)->prefilter = on != 0; }
 
 int orc_regex_match(const char* pattern, const char* input, size_t input_len) {
   try {

@@ -1,7 +1,11 @@
-// Differential fuzzer: libl7match's ECMAScript parser + DFA builder versus
+// Differential fuzzer: libl7match's ECMAScript parser + DFA builders (the
+// plain subset construction, the context / obligation construction for \b,
+// \B and look-ahead, and the packed field automaton of dfa_pack.h) versus
 // libstdc++ std::regex_match (the engine Envoy applies to HeaderMatcher
-// regexes, envoy/cilium_network_policy.h:68-71).  Test infrastructure only.
-//   fuzz_regex <seed> <n_patterns> <strings_per_pattern>
+// regexes, envoy/cilium_network_policy.h:68-71).  Patterns with
+// back-references are determinised as a superset (lower_for_dfa): the DFA
+// must accept everything std::regex accepts.  Test infrastructure only.
+//   fuzz_regex <seed> <n_patterns> <strings_per_pattern> [assertions 0/1]
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -9,11 +13,14 @@
 #include <string>
 #include <vector>
 
+#include "../../cilium_amd/csrc/dfa_pack.h"
 #include "../../cilium_amd/csrc/regex_ecma.h"
 
 using namespace l7m::re;
 static std::mt19937_64 rng;
 static int rnd(int n) { return (int)(rng() % (uint64_t)n); }
+static bool g_assert = false;  // generate \b \B (?=) (?!) and back-references
+static int g_groups = 0;       // capture groups opened so far in the pattern being generated
 
 static const char* kAtoms[] = {"a", "b", "c", "x", ".", "\\d", "\\w", "\\s", "\\D", "\\W", "\\S",
   "[ab]", "[^a]", "[a-c]", "[]", "[^]", "[\\d-]", "[-a]", "[a-]", "\\.", "/", "-", "_", "0", "9",
@@ -29,7 +36,10 @@ static std::string gen(int depth, bool* quant) {
   if (k < 4) s = kAtoms[rnd(sizeof(kAtoms) / sizeof(*kAtoms))];
   else if (k < 6) s = gen(depth + 1, &q1) + gen(depth + 1, &q2);
   else if (k < 7) s = gen(depth + 1, &q1) + "|" + gen(depth + 1, &q2);
-  else if (k < 8) s = "(" + gen(depth + 1, &q1) + ")";
+  else if (k < 8) {
+    ++g_groups;
+    s = "(" + gen(depth + 1, &q1) + ")";
+  }
   else if (k < 9) s = "(?:" + gen(depth + 1, &q1) + ")";
   else s = gen(depth + 1, &q1) + gen(depth + 1, &q2) + gen(depth + 1, &q3);
   *quant = q1 || q2 || q3;
@@ -41,11 +51,20 @@ static std::string gen(int depth, bool* quant) {
   }
   if (rnd(20) == 0) s = "^" + s;
   if (rnd(20) == 0) s = s + "$";
+  if (g_assert) {
+    if (rnd(6) == 0) s = (rnd(2) ? "\\b" : "\\B") + s;
+    if (rnd(6) == 0) s = s + (rnd(2) ? "\\b" : "\\B");
+    if (rnd(8) == 0) {
+      bool ql = false;
+      s = (rnd(2) ? "(?=" : "(?!") + gen(depth + 2, &ql) + ")" + s;
+    }
+    if (g_groups && rnd(10) == 0) s = s + "\\" + std::to_string(1 + rnd(g_groups));
+  }
   return s;
 }
 
 static std::string rand_input() {
-  static const char alpha[] = "abcxABZ09_ -./\t\n\r]}";
+  static const char alpha[] = "abcxABZ09_ -./\t\n\r]}aab";
   int n = rnd(8);
   std::string s;
   for (int i = 0; i < n; ++i) {
@@ -67,23 +86,32 @@ int main(int argc, char** argv) {
   rng.seed(argc > 1 ? strtoull(argv[1], 0, 10) : 1);
   int npat = argc > 2 ? atoi(argv[2]) : 2000;
   int nstr = argc > 3 ? atoi(argv[3]) : 200;
-  long checked = 0, mism = 0, unsup = 0, rejected = 0, parse_mism = 0;
+  g_assert = argc > 4 && atoi(argv[4]) != 0;
+  long checked = 0, mism = 0, unsup = 0, rejected = 0, parse_mism = 0, superset = 0, packed_mism = 0;
   for (int i = 0; i < npat; ++i) {
     bool qq = false;
+    g_groups = 0;
     std::string p = gen(0, &qq);
     if (getenv("FUZZ_TRACE")) { fprintf(stderr, "P %d %s\n", i, p.c_str()); }
     std::regex r;
     bool ok = true;
     try { r = std::regex(p, std::regex::ECMAScript | std::regex::optimize); } catch (...) { ok = false; }
-    Ast a; std::string err;
-    Status st = parse_ecma(p, &a, &err);
+    Ast full; std::string err;
+    Status st = parse_ecma(p, &full, &err);
     if (!ok) { rejected++; continue; }
     if (st == Status::Unsupported) { unsup++; continue; }
     if (st != Status::Ok) { parse_mism++; printf("PARSE-MISMATCH %s : %s\n", p.c_str(), err.c_str()); continue; }
+    bool exact = true;
+    Ast a = lower_for_dfa(full, &exact);
+    if (!exact) superset++;
     // Two-pattern DFA (pattern + a literal) also exercises multi-pattern sets.
     Ast lit = literal_ast("ab");
     Dfa d; DfaLimits lim;
-    if (build_dfa({&a, &lit}, lim, &d) != Status::Ok) { printf("BUILD-FAIL %s\n", p.c_str()); continue; }
+    lim.max_states = 1u << 16;
+    if (build_dfa({&a, &lit}, lim, &d) != Status::Ok) { unsup++; continue; }
+    // the packed field automaton (literal-prefix split, residual product)
+    l7m::PackedDfa pk;
+    const bool have_pk = l7m::build_field_dfa({&a, &lit}, l7m::FieldDfaLimits(), &pk) == Status::Ok;
     std::vector<std::string> ins;
     for (int j = 0; j < nstr; ++j) ins.push_back(rand_input());
     ins.push_back(""); ins.push_back("ab");
@@ -92,6 +120,23 @@ int main(int argc, char** argv) {
       bool got = dfa_match(d, s, 0);
       bool gotlit = dfa_match(d, s, 1);
       checked++;
+      if (have_pk) {
+        const uint32_t code = l7m::packed_walk(pk, reinterpret_cast<const uint8_t*>(s.data()), s.size());
+        bool pk0 = false;
+        if (code & l7m::kLatchedAccept) pk0 = (code & ~l7m::kLatchedAccept) == 0;
+        else for (uint32_t q : pk.sets[code]) pk0 |= q == 0;
+        if (pk0 != got) {
+          packed_mism++;
+          if (packed_mism < 10) printf("PACKED-MISMATCH pat=%s dfa=%d packed=%d\n", p.c_str(), got, pk0);
+        }
+      }
+      if (!exact) {  // superset automaton: every std::regex match must be accepted
+        if (ref && !got) {
+          mism++;
+          if (mism < 30) printf("SUPERSET-MISS pat=%s\n", p.c_str());
+        }
+        continue;
+      }
       if (ref != got || gotlit != (s == "ab")) {
         mism++;
         if (mism < 30) {
@@ -102,7 +147,7 @@ int main(int argc, char** argv) {
       }
     }
   }
-  printf("checked=%ld mismatches=%ld unsupported=%ld rejected_by_std=%ld parse_mismatch=%ld\n",
-         checked, mism, unsup, rejected, parse_mism);
-  return (mism || parse_mism) ? 1 : 0;
+  printf("checked=%ld mismatches=%ld unsupported=%ld rejected_by_std=%ld parse_mismatch=%ld superset=%ld "
+         "packed_mismatch=%ld\n", checked, mism, unsup, rejected, parse_mism, superset, packed_mism);
+  return (mism || parse_mism || packed_mism) ? 1 : 0;
 }

@@ -28,6 +28,7 @@ def _load():
     lib.orc_nfa_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_int]
     lib.orc_http_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
     lib.orc_http_free.argtypes = [P]
+    lib.orc_http_set_prefilter.argtypes = [P, ctypes.c_int]
     lib.orc_http_policies_new.argtypes = [ctypes.POINTER(L._NetworkPolicy), sz, ctypes.c_uint32,
                                           ctypes.POINTER(P), ctypes.c_char_p, sz]
     lib.orc_http_policies_eval.argtypes = [P, P, sz, P, sz, P, ctypes.c_int]
@@ -61,7 +62,10 @@ class HttpOracle:
     the Thompson-NFA / Pike-VM simulator (oracle/nfa.h), the long-input oracle
     for config 5 where the backtracker cannot finish or would overflow."""
 
-    def __init__(self, rules, dialect=L.DIALECT_ENVOY_ECMA_FULL, engine="std"):
+    def __init__(self, rules, dialect=L.DIALECT_ENVOY_ECMA_FULL, engine="std", prefilter=True):
+        """prefilter=False: every rule's matchers are evaluated per request, as
+        Envoy does (bench.py's cpu_baseline); the default skips rules whose
+        literal prefixes the request's values lack (same verdicts, faster)."""
         keep = []
         arr = (L._HttpRule * max(1, len(rules)))(*[L._http_rule_struct(r, keep) for r in rules])
         h = ctypes.c_void_p()
@@ -70,6 +74,7 @@ class HttpOracle:
         if rc != 0:
             raise OracleError(rc, err.value.decode(errors="replace"))
         self._h = h
+        _lib.orc_http_set_prefilter(h, 1 if prefilter else 0)
 
     def __del__(self, _free=_lib.orc_http_free):  # bound early: module globals are gone at exit
         if getattr(self, "_h", None) and self._h.value:

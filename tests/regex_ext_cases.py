@@ -1,0 +1,85 @@
+"""HTTP rules whose regexes use the ECMAScript constructs beyond the regular
+core that std::regex (the reference engine, envoy/cilium_network_policy.h:52-56,
+patterns passed verbatim by pkg/envoy/server.go:276-289) accepts: word
+boundaries \\b / \\B, look-ahead (?=X) / (?!X) and back-references \\k.
+Shared by the CPU (program interpreter) and GPU (kernel) parity tests; the
+oracle is std::regex_match itself (oracle/l7oracle.cc)."""
+import numpy as np
+
+from cilium_amd import l7match as L
+
+# Policies a user could write: word-delimited API versions, "anything but
+# admin", extension filters, repeated path segments.
+REALISTIC = [
+    L.PortRuleHTTP(Path=".*\\bv1\\b.*", Method="GET"),
+    L.PortRuleHTTP(Path="^(?!.*admin).*$", Method="POST"),
+    L.PortRuleHTTP(Path="/files/(?!secret)\\w+(\\.\\w+)?"),
+    L.PortRuleHTTP(Path=".*\\.(?!exe$)\\w+", Method="PUT"),
+    L.PortRuleHTTP(Path="/(?=[a-z]+/)[a-z]+/\\w*\\b"),
+    L.PortRuleHTTP(Method="(?!DELETE)[A-Z]+", Path="/ro/.*"),
+    L.PortRuleHTTP(Host="(?=.*\\.local$)svc\\d+\\..*"),
+    L.PortRuleHTTP(Path="/svc\\d+/v\\d+\\B.*", Headers=["x-tenant: t1"]),
+    L.PortRuleHTTP(Path="/(\\w+)/\\1(/.*)?"),                 # repeated segment (back-reference)
+    L.PortRuleHTTP(Path="/(a|bb)+-\\1"),                      # back-reference after a loop
+]
+
+ALPHA = list("ab/.-_xv1exmindEXs0 ")
+
+
+def _pat(rng, backrefs):
+    atoms = ["a", "b", "/", ".", "[a-c]", "[^/]", "\\d", "\\w", "\\W", "(x|yz)", "v1", "-", "\\b", "\\B"]
+    parts, groups = [], 0
+    for _ in range(int(rng.integers(1, 5))):
+        r = rng.random()
+        if r < 0.15:
+            inner = "".join(rng.choice(atoms[:10], size=int(rng.integers(1, 3))))
+            parts.append(("(?=" if rng.random() < 0.5 else "(?!") + inner + (".*" if rng.random() < 0.5 else "") + ")")
+        elif r < 0.25:
+            groups += 1
+            parts.append("(" + "".join(rng.choice(atoms[:10], size=int(rng.integers(1, 3)))) + ")" +
+                         str(rng.choice(["", "?", "+"])))
+        elif backrefs and groups and r < 0.32:
+            parts.append("\\%d" % int(rng.integers(1, groups + 1)))
+        else:
+            a = str(rng.choice(atoms))
+            q = "" if a in ("\\b", "\\B") else str(rng.choice(["", "*", "+", "?", "{0,2}"]))
+            parts.append(a + q)
+    s = "".join(parts)
+    return s if rng.random() > 0.1 else "^" + s + "$"
+
+
+def random_rules(rng, n, backrefs=False):
+    rules = []
+    for _ in range(n):
+        rules.append(L.PortRuleHTTP(Path=_pat(rng, backrefs) if rng.random() < 0.85 else "",
+                                    Method=str(rng.choice(["", "GET", "(?!POST)[A-Z]+", "\\bGET\\b"])),
+                                    Host=_pat(rng, backrefs) if rng.random() < 0.2 else ""))
+    return rules
+
+
+def random_requests(rng, n):
+    reqs = []
+    for _ in range(n):
+        path = "".join(rng.choice(ALPHA, size=int(rng.integers(0, 14))))
+        if rng.random() < 0.3:
+            path = str(rng.choice(["/files/", "/api/v1/", "/x/admin/", "/ro/", "/svc1/v2", "/ab/ab",
+                                   "/a-a", "/bb-bb", "/abb-bb"])) + path
+        reqs.append(L.HTTPRequest(str(rng.choice(["GET", "POST", "PUT", "DELETE"])), path,
+                                  "".join(rng.choice(ALPHA, size=int(rng.integers(0, 8)))),
+                                  [("x-tenant", "t1")] if rng.random() < 0.3 else []))
+    return reqs
+
+
+def realistic_requests(rng, n):
+    """Paths aimed at REALISTIC's patterns (hits and near misses)."""
+    pool = ["/api/v1/users", "/api/v10/users", "/api/v1", "/v1", "/xv1/", "/admin/x", "/x/admin", "/files/a.txt",
+            "/files/secret", "/files/secretx", "/files/a", "/up/a.exe", "/up/a.exe2", "/up/a.txt", "/abc/def",
+            "/abc/", "/ro/x", "/svc1/v22", "/svc1/v2", "/users/users", "/users/users/x", "/a/b", "/a-a", "/bb-bb",
+            "/aab-b", "/abb-bb", "/ab-ab"]
+    hosts = ["svc1.ns.local", "svc1.ns.localx", "svcx.local", "svc12.a.local", ""]
+    reqs = []
+    for _ in range(n):
+        reqs.append(L.HTTPRequest(str(rng.choice(["GET", "POST", "PUT", "DELETE", "PATCH"])), str(rng.choice(pool)),
+                                  str(rng.choice(hosts)) or None,
+                                  [("x-tenant", "t1")] if rng.random() < 0.5 else []))
+    return reqs

@@ -9,6 +9,8 @@ import subprocess
 import numpy as np
 import pytest
 
+import regex_ext_cases as X
+
 from cilium_amd import l7match as L
 from cilium_amd import workloads as W
 from oracle import HttpOracle, OracleError, regex_match
@@ -91,10 +93,24 @@ def test_invalid_regex_nacks_and_unsupported_is_explicit():
         assert e.value.code == L.L7M_EINVAL_REGEX, bad
         with pytest.raises(OracleError):
             HttpOracle([L.PortRuleHTTP(Path=bad)])
-    for unsup in ("(a)\\1", "\\bfoo", "(?=a)a", "a(?!b)"):
-        with pytest.raises(L.L7Error) as e:
-            L.RuleSet.compile_http([L.PortRuleHTTP(Path=unsup)])
-        assert e.value.code == L.L7M_EUNSUPPORTED, unsup
+    # \\b, \\B and look-ahead compile (exact automata, regex_ecma.cc build_ctx)
+    for ok in ("\\bfoo", "(?=a)a", "a(?!b)", "x\\B"):
+        L.RuleSet.compile_http([L.PortRuleHTTP(Path=ok)])
+
+
+def test_word_boundary_and_lookahead_rules_match_oracle():
+    """Realistic and random rule sets with \\b / \\B / (?=) / (?!) through the
+    program interpreter (the kernel's algorithm) against std::regex_match."""
+    rng = np.random.default_rng(5)
+    rules = [r for r in X.REALISTIC if "\\1" not in r.Path]
+    reqs = X.realistic_requests(rng, 3000) + X.random_requests(rng, 2000)
+    arena, offs = L.pack_http(reqs)
+    v = _interp_vs_oracle(rules, arena, offs)
+    assert len(set(v.tolist())) >= 6
+    for trial in range(12):
+        rules = X.random_rules(rng, int(rng.integers(1, 16)))
+        arena, offs = L.pack_http(X.random_requests(rng, 1500))
+        _interp_vs_oracle(rules, arena, offs)
 
 
 def test_unknown_dialect_is_rejected():
@@ -209,11 +225,17 @@ def test_regex_compiler_differential_fuzz():
     builder against std::regex_match on random patterns and inputs."""
     exe = "/tmp/l7m_fuzz_regex"
     src = os.path.join(ROOT, "tests", "cpp", "fuzz_regex.cc")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", exe, src,
-                           os.path.join(ROOT, "cilium_amd", "csrc", "regex_ecma.cc")])
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-o", exe, src,
+                           os.path.join(ROOT, "cilium_amd", "csrc", "regex_ecma.cc"),
+                           os.path.join(ROOT, "cilium_amd", "csrc", "dfa_pack.cc")])
     out = subprocess.run(["timeout", "240", exe, "7", "600", "120"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout[-3000:]
     assert "mismatches=0" in out.stdout
+    # word boundaries, look-ahead (exact) and back-references (superset automata)
+    for seed in ("11", "12"):
+        out = subprocess.run(["timeout", "240", exe, seed, "3000", "100", "1"], capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout[-3000:]
+        assert "mismatches=0" in out.stdout and "packed_mismatch=0" in out.stdout
 
 
 def test_compiler_table_only_lds_placement_matches_oracle():
