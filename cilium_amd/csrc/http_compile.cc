@@ -30,6 +30,7 @@
 #include "l7m_internal.h"
 #include "program.h"
 #include "regex_ecma.h"
+#include "regex_vm.h"
 
 namespace l7m {
 namespace {
@@ -326,12 +327,16 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   if (opts.max_dfa_states) lim.max_multi_states = opts.max_dfa_states;
   if (opts.max_table_bytes) lim.max_slots = std::min<uint64_t>(lim.max_slots, opts.max_table_bytes / 4);
   std::vector<std::vector<Group>> groups(nf);
+  // slow-path programs (regex_vm.h) of the patterns whose automata are
+  // supersets (back-references, oversized look-ahead): [field][pattern]
+  std::vector<std::vector<std::vector<uint32_t>>> slow_vm(nf);
   // field pattern -> (group, local id)
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fp_loc(nf);
   for (uint32_t f = 0; f < nf; ++f) {
     if (fpats[f].empty()) continue;
     std::vector<re::Ast> asts(fpats[f].size());
     std::vector<const re::Ast*> ptrs;
+    slow_vm[f].resize(fpats[f].size());
     for (size_t p = 0; p < fpats[f].size(); ++p) {
       const auto& fp = fpats[f][p];
       if (fp.kind == MatchKind::Regex && re2) {
@@ -372,8 +377,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
             exact = false;
           }
         }
-        if (!exact)
-          return fail(L7M_EUNSUPPORTED, "regex '" + fp.value + "': back-reference (slow path not built)");
+        if (!exact) {
+          // the automaton accepts a superset; rules using this pattern are
+          // decided by the slow path (libstdc++'s executor restated)
+          std::string verr;
+          if (!vm_compile(full, &slow_vm[f][p], &verr))
+            return fail(L7M_ETOOBIG, "regex '" + fp.value + "': " + verr);
+        }
       } else {
         asts[p] = re::literal_ast(fp.value);
       }
@@ -486,6 +496,19 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     }
   }
 
+  // rules with slow-path matchers: (field, program) pairs, in matcher order
+  std::vector<uint8_t> slow_rule(n, 0);
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> slow_list(n);  // (field, pattern)
+  uint32_t n_slow = 0;
+  for (size_t i = 0; i < n; ++i) {
+    for (const auto& m : rule_m[i])
+      if (m.fpat != kNone && !slow_vm[m.field][m.fpat].empty()) slow_list[i].push_back({m.field, m.fpat});
+    if (!slow_list[i].empty()) {
+      slow_rule[i] = 1;
+      ++n_slow;
+    }
+  }
+
   // ---- assemble the program -------------------------------------------
   std::vector<uint32_t> pool;  // set pattern lists, remote ids
   auto push_list = [&](const std::vector<uint32_t>& v) -> Span {
@@ -500,7 +523,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     for (uint32_t rid : rids) {
       cr.push_back(rid);
       cr.push_back(static_cast<uint32_t>(rule_m[rid].size()) | plan.rule_entry[rid] << kCrEntryShift |
-                   (remotes[rid].empty() ? 0u : kCrRemote));
+                   (remotes[rid].empty() ? 0u : kCrRemote) | (slow_rule[rid] ? kCrSlow : 0u));
       for (const auto& m : rule_m[rid]) {
         uint32_t dfa = 0, pat = 0;
         if (m.fpat != kNone) {
@@ -763,6 +786,30 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   }
   h.n_policies = plan.n_policies;
   h.pair_pa = 0;  // (unused; the paired walk measured slower, profiles/r03/ab_round3.md)
+  // slow path: Span[n_rules] into the pool of (field, program offset) pairs,
+  // then the programs
+  h.off_slow = kNone;
+  h.n_slow = n_slow;
+  std::vector<std::vector<uint32_t>> slow_off(nf);
+  std::vector<Span> slow_span(n, Span{0, 0});
+  if (n_slow) {
+    h.off_slow = take(2ull * n);
+    for (uint32_t f = 0; f < nf; ++f) {
+      slow_off[f].assign(fpats[f].size(), kNone);
+      for (size_t pi = 0; pi < fpats[f].size(); ++pi)
+        if (!slow_vm[f][pi].empty()) slow_off[f][pi] = take(slow_vm[f][pi].size());
+    }
+    for (size_t i = 0; i < n; ++i) {
+      if (slow_list[i].empty()) continue;
+      std::vector<uint32_t> pr;
+      for (const auto& fp : slow_list[i]) {
+        pr.push_back(fp.first);
+        pr.push_back(slow_off[fp.first][fp.second]);
+      }
+      slow_span[i] = push_list(pr);
+      slow_span[i].len /= 2;  // pairs
+    }
+  }
   for (uint32_t k = 0; k < ndfa; ++k) h.search |= dd[k].kind == kDfaSearch ? 1u : 0u;
   h.ent_mask = ent_slots - 1;
   h.ent_tab_off = take(2ull * ent_slots);
@@ -914,6 +961,14 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   if (n) std::memcpy(P + h.off_remotes, rremote.data(), rremote.size() * sizeof(Span));
   if (!pool.empty()) std::memcpy(P + h.off_pool, pool.data(), pool.size() * 4);
   if (!cr.empty()) std::memcpy(P + h.off_cr, cr.data(), cr.size() * 4);
+  if (n_slow) {
+    Span* sl = reinterpret_cast<Span*>(P + h.off_slow);
+    for (uint32_t f = 0; f < nf; ++f)
+      for (size_t pi = 0; pi < fpats[f].size(); ++pi)
+        if (slow_off[f][pi] != kNone)
+          std::memcpy(P + slow_off[f][pi], slow_vm[f][pi].data(), slow_vm[f][pi].size() * 4);
+    for (size_t i = 0; i < n; ++i) sl[i] = slow_span[i];
+  }
 
   res.program = std::move(prog);
   res.info.proto = L7M_PROTO_HTTP;

@@ -27,6 +27,7 @@
 #include "../../include/l7match.h"
 #include "l7m_device.h"
 #include "program.h"
+#include "regex_vm.h"
 
 namespace l7m {
 namespace {
@@ -485,6 +486,46 @@ struct WalkOut {
   bool h0;            // the port-0 entry has HTTP rules
 };
 constexpr int32_t kNeedVerify = INT32_MIN;
+// First pass: the request's smallest candidate may be a slow-path rule
+// (kCrSlow): it is queued for http_slow_kernel, which decides it exactly.
+constexpr int32_t kDeferred = INT32_MIN + 1;
+
+// Where field f's value lies in a record (slow pass): the pseudo headers from
+// the fixed part, other fields as the first header whose name maps to f (the
+// walk phase's header-name lookup).  false if absent.
+template <class Src>
+__device__ bool field_at(const Ctx& c, const HttpHeader& h, const Src& src, uint32_t f, uint32_t* pos,
+                         uint32_t* len) {
+  const uint32_t w2 = src.word(2), w3 = src.word(3), w4 = src.word(4);
+  const uint32_t flags = (w2 >> 16) & 0xffu, nhdr = w2 >> 24;
+  const uint32_t mlen = w3 & 0xffffu, plen = w3 >> 16, alen = w4 & 0xffffu;
+  uint32_t p = L7M_HTTP_REC_FIXED + 4u * nhdr;
+  if (f < 3) {
+    if (!(flags & (f == 0 ? L7M_HTTP_F_METHOD : f == 1 ? L7M_HTTP_F_PATH : L7M_HTTP_F_AUTHORITY))) return false;
+    *pos = p + (f >= 1 ? mlen : 0u) + (f == 2 ? plen : 0u);
+    *len = f == 0 ? mlen : f == 1 ? plen : alen;
+    return true;
+  }
+  p += mlen + plen + alen;
+  for (uint32_t j = 0; j < nhdr; ++j) {
+    const uint32_t e = src.word(5 + j), nl = e & 0xffffu, vl = e >> 16;
+    uint32_t g = kNone;
+    if (h.lds_name_tab != kNone) {
+      g = name_field_of(c, h, src, p, nl);
+    } else {
+      const uint32_t code = walk_dfa<false, false>(c, h.n_dfas, src, p, nl);
+      if (code & kLatchedBit) g = 3u + (code & ~kLatchedBit);
+      else if (code) g = c.name_field[code];
+    }
+    if (g == f) {
+      *pos = p + nl;
+      *len = vl;
+      return true;
+    }
+    p += nl + vl;
+  }
+  return false;
+}
 
 // Walk phase of one record whose first `limit` bytes are readable: record
 // validation, port-entry selection and every DFA walk.  Returns the verdict
@@ -631,8 +672,13 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
 // Verification phase: the first rule (smallest index) among the keyed
 // candidates whose other matchers, port entry and remote set hold; the
 // check-record lists are selected by the walks' end codes.
-template <int kReg>
-__device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o) {
+// kSlowPass (http_slow_kernel): rules with slow-path matchers (kCrSlow) are
+// decided by the executor of regex_vm.h on the record's field values (src,
+// vm: this lane's scratch); in the first pass such a rule whose automaton
+// checks pass only marks the request for deferral.
+template <int kReg, bool kSlowPass = false, class Src = GlbSrc>
+__device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o,
+                                               const Src* src = nullptr, uint32_t* vm = nullptr) {
   const Codes<kReg>& codes = o.codes;
   const uint64_t present = o.present;
   asm volatile("" ::"v"(o.pf_t));  // the touch completes here, not at its first use
@@ -646,6 +692,38 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
   const bool masked = h.n_dfas <= 64;
   const uint64_t cand_all = masked ? ((static_cast<uint64_t>(h.cand_dfas_hi) << 32) | h.cand_dfas_lo) : 0;
   uint32_t best = h.always_rule;
+  uint32_t min_slow = kNone;   // first pass: smallest slow-path rule whose automaton checks passed
+  uint32_t min_limit = kNone;  // slow pass: smallest rule whose evaluation hit the executor's limits
+  // A candidate whose checks passed: rules with slow-path matchers are
+  // deferred (first pass) or run through the executor (slow pass).
+  auto take = [&](uint32_t rid, uint32_t hd) -> bool {
+    if (!(hd & kCrSlow)) {
+      best = rid;
+      return true;
+    }
+    if constexpr (!kSlowPass) {
+      min_slow = rid < min_slow ? rid : min_slow;
+      return false;
+    } else {
+      const uint32_t* sl = c.prog + h.off_slow + 2u * rid;
+      const uint32_t so = sl[0], sn = sl[1];
+      bool all = true;
+      for (uint32_t q = 0; q < sn && all; ++q) {
+        const uint32_t f = c.pool[so + 2 * q], off = c.pool[so + 2 * q + 1];
+        uint32_t pos = 0, len = 0;
+        if (!field_at(c, h, *src, f, &pos, &len)) {
+          all = false;
+          break;
+        }
+        const int r = vm_match(c.prog + off, reinterpret_cast<const uint8_t*>(src->w) + pos, len, vm,
+                               kVmScratchWords, kVmMaxSteps);
+        if (r == kVmLimit) min_limit = rid < min_limit ? rid : min_limit;
+        all = r == kVmMatched;
+      }
+      if (all) best = rid;
+      return all;
+    }
+  };
   auto remote_ok = [&](uint32_t rid) -> bool {  // PortNetworkPolicyRule::Matches (h:92-97)
     const uint32_t* rp = reinterpret_cast<const uint32_t*>(c.remotes + rid);
     uint32_t roff = gld(rp), rlen = gld(rp + 1);
@@ -677,10 +755,7 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
         if (!((present >> f) & 1ull)) ok = false;
         else if (!((a >> 8) & 1u)) ok = code_has<(kReg < 0)>(c, a >> 9, codes.get(a >> 9), pat);
       }
-      if (ok) {
-        best = rid;
-        break;
-      }
+      if (ok && take(rid, rw[1])) break;
       o += 2 + 2 * nm;
     }
   };
@@ -740,7 +815,7 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
           }
         }
       }
-      if (ok) best = rid;
+      if (ok) take(rid, hd);
     } else {
       scan(Span{q0.y, len});
     }
@@ -799,6 +874,8 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
   }
   if (h.zero_list.len) scan(h.zero_list);
 
+  if (!kSlowPass && min_slow < best) return kDeferred;
+  if (kSlowPass && min_limit < best) return L7M_VERDICT_UNSUPPORTED;  // undecided before the first match
   if (best != kNone) return static_cast<int32_t>(best);
   // the exact-port entry matched nothing; a port-0 entry without HTTP rules allows
   return h0 ? L7M_VERDICT_DENY : L7M_VERDICT_ALLOW_NO_L7;
@@ -842,7 +919,7 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
                                                            const uint64_t* __restrict__ offs, uint64_t n,
                                                            int32_t* __restrict__ verdicts,
                                                            unsigned long long* __restrict__ hits, uint32_t stage,
-                                                           uint32_t* __restrict__ scratch) {
+                                                           uint32_t* __restrict__ scratch, uint32_t* __restrict__ slowq) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -993,13 +1070,17 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     if (lane < take) {
       if (v == kNeedVerify) v = eval_verify<kReg>(c, h, wo);
       verdicts[t.cur + lane] = v;
+      if (v == kDeferred) {  // decided by http_slow_kernel (rules with slow-path matchers)
+        const uint32_t at = atomicAdd(slowq, 1u);
+        slowq[1 + at] = static_cast<uint32_t>(t.cur + lane);
+      }
     }
     qtn(4);
     if constexpr (kProf) prof_tile += __builtin_amdgcn_s_memtime() - te0;
     if (kHits != kNoHits) {
       uint32_t slot = kNone;
       // allows decided without a rule (no L7 rules, no port policy) are not counted
-      if (lane < take && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY)
+      if (lane < take && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY && v != kDeferred)
         slot = v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u);
       if (kHits == kLdsHits) {
         // denies / errors are common: one add per wave for them
@@ -1043,6 +1124,61 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
   }
 }
 
+// Second pass over the requests the first pass deferred (a slow-path rule may
+// decide them, program.h kCrSlow): one lane per queued request, records read
+// from HBM, the same walk phase, then verification with the slow-path
+// executor (regex_vm.h) on this lane's scratch.  Verdicts and counters of
+// these requests are written here only.
+constexpr uint32_t kSlowBlocks = 4;  // 4096 lanes x kVmScratchWords words of executor scratch
+template <int kReg, bool kLit>
+__global__ __launch_bounds__(kBlock) void http_slow_kernel(const uint32_t* __restrict__ prog,
+                                                           const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                           const uint64_t* __restrict__ offs, uint64_t n,
+                                                           int32_t* __restrict__ verdicts,
+                                                           unsigned long long* __restrict__ hits,
+                                                           const uint32_t* __restrict__ slowq,
+                                                           uint32_t* __restrict__ vmscratch) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
+  const uint32_t tid = threadIdx.x;
+  uint32_t* img = smem;
+  {
+    const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
+    uint4* l = reinterpret_cast<uint4*>(img);
+    for (uint32_t i = tid; i < h.lds_image_words / 4u; i += kBlock) l[i] = g[i];
+  }
+  __syncthreads();
+  Ctx c;
+  c.prog = prog;
+  c.img = img;
+  c.dds = reinterpret_cast<const DfaDesc*>(img + h.lds_dfas);
+  c.fields = reinterpret_cast<const FieldDesc*>(img + h.lds_fields);
+  c.name_field = img + h.lds_name_field;
+  c.sets = reinterpret_cast<const Span*>(prog + h.off_sets);
+  c.pool = prog + h.off_pool;
+  c.cr = prog + h.off_cr;
+  c.remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
+  const uint32_t gtid = blockIdx.x * kBlock + tid;
+  uint32_t* vm = vmscratch + static_cast<uint64_t>(gtid) * kVmScratchWords;
+  const uint32_t nq = slowq[0];
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t q = gtid; q < nq; q += gridDim.x * kBlock) {
+    const uint32_t ri = slowq[1 + q];
+    if (ri >= n) continue;
+    const uint64_t o = offs[ri];
+    WalkOut<kReg> wo;
+    if constexpr (!kReg) wo.codes.p = img + h.lds_image_words + tid;
+    int32_t v = L7M_VERDICT_PARSE_ERROR;
+    const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
+    const GlbSrc src{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
+    if (inb) v = eval_walk<kReg, 0, kLit>(c, h, src, arena_bytes - o, wo, prof);
+    if (v == kNeedVerify) v = eval_verify<kReg, true>(c, h, wo, &src, vm);
+    verdicts[ri] = v;
+    if (hits && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY)
+      atomicAdd(hits + (v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u)), 1ull);
+  }
+}
+
 }  // namespace
 
 size_t http_lds_bytes(const HttpHeader& h, uint32_t stage) {
@@ -1064,14 +1200,27 @@ uint32_t http_stage_bytes(const HttpHeader& h) {
 template <int kHits, int kReg, int kAblate = 0, bool kLit = false>
 static hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                       unsigned long long* hits, uint32_t stage, uint32_t* scratch = nullptr) {
+                       unsigned long long* hits, uint32_t stage, uint32_t* scratch = nullptr,
+                       uint32_t* slowq = nullptr) {
   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU); set per device
   // and instantiation, thread-safely (l7m_device.h)
   const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate, kLit>),
                                          kHttpLdsBytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate, kLit>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
-                     offs, n, verdicts, hits, stage, scratch);
+                     offs, n, verdicts, hits, stage, scratch, slowq);
+  return hipGetLastError();
+}
+
+template <int kReg, bool kLit>
+static hipError_t launch_slow(const HttpHeader& h, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
+                              uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
+                              unsigned long long* hits, const uint32_t* slowq, uint32_t* vmscratch) {
+  const size_t lds = 4u * (static_cast<size_t>(h.lds_image_words) + (kReg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock));
+  const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_slow_kernel<kReg, kLit>), kHttpLdsBytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((http_slow_kernel<kReg, kLit>), dim3(kSlowBlocks), dim3(kBlock), lds, stream, dprog, arena,
+                     arena_bytes, offs, n, verdicts, hits, slowq, vmscratch);
   return hipGetLastError();
 }
 
@@ -1115,23 +1264,53 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   }
   // end codes in 4 or 8 registers, or in LDS columns
   const bool lit = (flags & kLaunchLiterals) != 0;
-#define L7M_LAUNCH(M, R)                                                                                         \
-  {                                                                                                              \
-    if (lit) return launch_one<M, R, 0, true>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts,   \
-                                              hits, stage);                                                      \
-    return launch_one<M, R>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);       \
+  const int R = h.n_dfas <= 4 ? 4 : reg ? 8 : 0;
+  // programs with slow-path rules (program.h kCrSlow): the first pass queues
+  // the requests they may decide, http_slow_kernel decides them; the queue
+  // (count + up to n indices) and the executor scratch are stream-ordered
+  uint32_t* slowq = nullptr;
+  uint32_t* vms = nullptr;
+  const size_t qbytes = (4ull * (n + 1) + 255) & ~size_t(255);
+  if (h.n_slow) {
+    void* buf = nullptr;
+    const size_t vbytes = static_cast<size_t>(kSlowBlocks) * kBlock * kVmScratchWords * 4u;
+    hipError_t e = hipMallocAsync(&buf, qbytes + vbytes, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(buf, 0, 4, stream);
+    if (e != hipSuccess) return e;
+    slowq = static_cast<uint32_t*>(buf);
+    vms = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + qbytes);
   }
-#define L7M_LAUNCH_R(M)                 \
-  {                                     \
-    if (h.n_dfas <= 4) L7M_LAUNCH(M, 4); \
-    if (reg) L7M_LAUNCH(M, 8);          \
-    L7M_LAUNCH(M, 0);                   \
+  hipError_t e = hipSuccess;
+#define L7M_LAUNCH(M, RR)                                                                                          \
+  e = lit ? launch_one<M, RR, 0, true>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage, \
+                                       nullptr, slowq)                                                             \
+          : launch_one<M, RR>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage, nullptr, \
+                              slowq)
+#define L7M_LAUNCH_M(RR)                                      \
+  {                                                           \
+    if (mode == kNoHits) L7M_LAUNCH(kNoHits, RR);             \
+    else if (mode == kLdsHits) L7M_LAUNCH(kLdsHits, RR);      \
+    else L7M_LAUNCH(kGlobalHits, RR);                         \
   }
-  if (mode == kNoHits) L7M_LAUNCH_R(kNoHits);
-  if (mode == kLdsHits) L7M_LAUNCH_R(kLdsHits);
-  L7M_LAUNCH_R(kGlobalHits);
-#undef L7M_LAUNCH_R
+  if (R == 4) L7M_LAUNCH_M(4)
+  else if (R == 8) L7M_LAUNCH_M(8)
+  else L7M_LAUNCH_M(0)
+#undef L7M_LAUNCH_M
 #undef L7M_LAUNCH
+  if (h.n_slow) {
+#define L7M_SLOW(RR)                                                                                              \
+  e = lit ? launch_slow<RR, true>(h, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq, vms)     \
+          : launch_slow<RR, false>(h, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq, vms)
+    if (e == hipSuccess) {
+      if (R == 4) L7M_SLOW(4);
+      else if (R == 8) L7M_SLOW(8);
+      else L7M_SLOW(0);
+    }
+#undef L7M_SLOW
+    const hipError_t e2 = hipFreeAsync(slowq, stream);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
 }
 
 }  // namespace l7m

@@ -154,6 +154,11 @@ struct FieldDesc {
 //   then per matcher: [field | kind << 8 | dfa << 9] [pattern]
 // kind 0 = the DFA's end code must contain `pattern`, 1 = field present.
 constexpr uint32_t kCrRemote = 0x80000000u;
+// The rule has matchers whose automata accept a superset (back-references,
+// look-ahead past its automaton limit): when its other checks pass, the
+// request is decided by the slow path (regex_vm.h) -- the first pass defers
+// it, http_slow_kernel evaluates it exactly.
+constexpr uint32_t kCrSlow = 0x40000000u;
 constexpr uint32_t kCrEntryShift = 8;
 constexpr uint32_t kCrMaxMatchers = 255;
 constexpr uint32_t kCrMaxEntries = 1u << 22;
@@ -207,8 +212,10 @@ struct HttpHeader {
   uint32_t pres_fields_lo; // bit f: field f has a presence-keyed check-record list
   uint32_t pres_fields_hi;
   uint32_t search;         // 1: some value DFA is a kDfaSearch automaton (RE2 dialect)
-  uint32_t pair_pa;        // 1: :path and :authority have one LDS-walked DFA each (paired walk)
-  uint32_t pad[2];         // header = 40 words
+  uint32_t pair_pa;        // (unused, 0)
+  uint32_t off_slow;       // Span[n_rules] into the pool: (field, slow program offset) pairs of the
+                           // rules with kCrSlow matchers (regex_vm.h), or kNone
+  uint32_t n_slow;         // rules with slow-path matchers
 };
 // Header-name table (LDS image): exact lower-case header names of the rules
 // -> field id, open addressing on the program.h name hash; slot =

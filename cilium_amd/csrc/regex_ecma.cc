@@ -377,7 +377,9 @@ class Parser {
       const bool lazy = match(T_OPT);
       if (mx >= 0 && mx < static_cast<long long>(mn)) fail(Status::Syntax, "bad brace range");
       if (mn > 100000 || mx > 100000) fail(Status::TooBig, "repeat count");
-      return rep(a, static_cast<int>(mn), static_cast<int>(mx), lazy);
+      const int r = rep(a, static_cast<int>(mn), static_cast<int>(mx), lazy);
+      ast_.nodes[r].brace = true;
+      return r;
     }
     return -1;
   }

@@ -38,6 +38,7 @@ struct Node {
                           // WordB / Look: min = 1 for the negated form (\B, (?!X))
                           // Group / Backref: min = capture index (1-based)
   bool lazy = false;      // Rep: non-greedy ('?' after the quantifier; exploration order only)
+  bool brace = false;     // Rep: written {n}, {n,} or {n,m} (libstdc++ builds those from copies)
 };
 
 struct Ast {
@@ -108,4 +109,9 @@ void make_search_prefix(Ast* a);
 void simplify_search(Ast* a);
 
 }  // namespace re
+
+// The slow path's program for a full AST (regex_vm.cc, executed by
+// regex_vm.h vm_match); false (with *err) past its size limit.
+bool vm_compile(const re::Ast& full, std::vector<uint32_t>* out, std::string* err);
+
 }  // namespace l7m

@@ -15,6 +15,7 @@
 
 #include "../../cilium_amd/csrc/dfa_pack.h"
 #include "../../cilium_amd/csrc/regex_ecma.h"
+#include "../../cilium_amd/csrc/regex_vm.h"
 
 using namespace l7m::re;
 static std::mt19937_64 rng;
@@ -88,6 +89,8 @@ int main(int argc, char** argv) {
   int nstr = argc > 3 ? atoi(argv[3]) : 200;
   g_assert = argc > 4 && atoi(argv[4]) != 0;
   long checked = 0, mism = 0, unsup = 0, rejected = 0, parse_mism = 0, superset = 0, packed_mism = 0;
+  long vm_checked = 0, vm_mism = 0, vm_limit = 0;
+  std::vector<uint32_t> scratch(1u << 16);
   for (int i = 0; i < npat; ++i) {
     bool qq = false;
     g_groups = 0;
@@ -101,6 +104,11 @@ int main(int argc, char** argv) {
     if (!ok) { rejected++; continue; }
     if (st == Status::Unsupported) { unsup++; continue; }
     if (st != Status::Ok) { parse_mism++; printf("PARSE-MISMATCH %s : %s\n", p.c_str(), err.c_str()); continue; }
+    // the slow path (libstdc++'s executor restated) must equal std::regex on
+    // every pattern, back-references included
+    std::vector<uint32_t> vprog;
+    std::string verr;
+    const bool have_vm = l7m::vm_compile(full, &vprog, &verr);
     bool exact = true;
     Ast a = lower_for_dfa(full, &exact);
     if (!exact) superset++;
@@ -117,6 +125,21 @@ int main(int argc, char** argv) {
     ins.push_back(""); ins.push_back("ab");
     for (const auto& s : ins) {
       bool ref = std::regex_match(s, r);
+      if (have_vm) {
+        const int v = l7m::vm_match(vprog.data(), reinterpret_cast<const uint8_t*>(s.data()),
+                                    static_cast<uint32_t>(s.size()), scratch.data(),
+                                    static_cast<uint32_t>(scratch.size()), 1u << 22);
+        ++vm_checked;
+        if (v == l7m::kVmLimit) ++vm_limit;
+        else if ((v == l7m::kVmMatched) != ref) {
+          ++vm_mism;
+          if (vm_mism < 20) {
+            printf("VM-MISMATCH pat=%s in=", p.c_str());
+            for (unsigned char ch : s) printf("\\x%02x", ch);
+            printf(" ref=%d vm=%d\n", ref, v);
+          }
+        }
+      }
       bool got = dfa_match(d, s, 0);
       bool gotlit = dfa_match(d, s, 1);
       checked++;
@@ -148,6 +171,7 @@ int main(int argc, char** argv) {
     }
   }
   printf("checked=%ld mismatches=%ld unsupported=%ld rejected_by_std=%ld parse_mismatch=%ld superset=%ld "
-         "packed_mismatch=%ld\n", checked, mism, unsup, rejected, parse_mism, superset, packed_mism);
-  return (mism || parse_mism || packed_mism) ? 1 : 0;
+         "packed_mismatch=%ld vm_checked=%ld vm_mismatch=%ld vm_limit=%ld\n", checked, mism, unsup, rejected,
+         parse_mism, superset, packed_mism, vm_checked, vm_mism, vm_limit);
+  return (mism || parse_mism || packed_mism || vm_mism || vm_limit) ? 1 : 0;
 }

@@ -7,11 +7,18 @@ LDS candidate tables are checked too).  This lets the rule COMPILER (regex ->
 packed DFA groups, check records) be checked against the CPU oracle without a
 GPU; the kernel itself is checked on the GPU by the -m gpu tests.  Small
 inputs only (pure-Python loops)."""
+import ctypes
+import os
 import struct
 
 import numpy as np
 
 from cilium_amd import l7match as L
+
+_VM = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "bin", "libvmhost.so"))
+_VM.vm_host_match.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+VM_SCRATCH_WORDS, VM_MAX_STEPS = 8192, 1 << 22  # regex_vm.h kVmScratchWords / kVmMaxSteps
+CR_SLOW = 0x40000000  # program.h kCrSlow
 
 KNONE = 0xFFFFFFFF
 LATCHED = 0x80000000
@@ -21,12 +28,10 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
               "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi "
-              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search pair_pa").split()
+              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search pair_pa off_slow n_slow").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab "
               "lds_skip skip_lim kind acc_cmap_off acc_mid_off acc_ncls").split()
-SKIP_LOOP, SKIP_LIT = 1, 2  # program.h kSkipLoop / kSkipLit
-SKIP_MIN_REST = 64  # l7m_kernels.hip kSkipMinRest: bytes left for a skip row to be taken
 ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 DFA_WORDS = 32  # sizeof(DfaDesc) / 4
 DFA_SEARCH = 1  # program.h kDfaSearch
@@ -48,13 +53,13 @@ def name_hash(data: bytes) -> int:
 
 
 class HttpProgram:
-    def __init__(self, prog: np.ndarray, skips: bool = True):
-        self.skips = skips  # follow the kernel's skip rows (dfa_pack.h) at 8-byte block boundaries
+    def __init__(self, prog: np.ndarray):
+        self.prog = np.ascontiguousarray(prog, dtype=np.uint32)
         self.w = prog.astype(np.uint64).astype(np.int64).tolist()
         self.h = dict(zip(HDR_FIELDS, self.w[:len(HDR_FIELDS)]))
         h = self.h
         assert h["magic"] == 0x3448374C
-        assert len(HDR_FIELDS) == 38  # + 2 pad words (program.h HttpHeader, 40 words)
+        assert len(HDR_FIELDS) == 40  # program.h HttpHeader, 40 words
         io = h["lds_image_off"]
         self.img = self.w[io:io + h["lds_image_words"]]
         self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
@@ -109,7 +114,6 @@ class HttpProgram:
             # LDS copy (program.h kLdsRowShift): e = (image row index << 16) |
             # es8 << 8 | label, the table's row 0 is the dead row
             t0 = d["lds_table"]
-            slim = (d["skip_lim"] & 0xFFFF) if (self.skips and d["lds_skip"] != KNONE) else None
             n = len(data)
             st = [base, es8, last]
 
@@ -121,42 +125,7 @@ class HttpProgram:
                     st[2] = slot
                 st[0], st[1] = ((e >> 16) - t0, (e >> 8) & 0xFF) if (e & 0xFF) == c else (0, 0)
 
-            def skip(k):  # l7m_kernels.hip LdsChain::skip
-                for _ in range(64):
-                    bs = st[0]
-                    if bs < slim or not bs or k >= n:
-                        return k
-                    sk = d["lds_skip"]
-                    w = self.img[sk + bs - slim]
-                    if w & SKIP_LOOP:
-                        if any((self.img[t0 + bs + c] & 0xFF) != c for c in data[k:]):
-                            st[0] = 0
-                        return n
-                    if not (w & SKIP_LIT):
-                        return k
-                    ln, off, tslot = (w >> 2) & 31, (w >> 7) & 511, w >> 16
-                    if n - k < ln:
-                        st[0] = 0
-                        return n
-                    lw = sk - (d["skip_lim"] >> 16)
-                    pool = b"".join(int(x).to_bytes(4, "little") for x in self.img[lw:sk])
-                    if data[k:k + ln] != pool[off:off + ln]:
-                        st[0] = 0
-                        return n
-                    e = self.img[t0 + tslot]
-                    st[0], st[1] = (e >> 16) - t0, (e >> 8) & 0xFF
-                    k += ln
-                return k
-
             k = 0
-            if base and slim is not None:
-                while k + 8 <= n and st[0]:
-                    for c in data[k:k + 8]:
-                        if st[0]:
-                            step(c)
-                    k += 8
-                    if st[0] and st[0] >= slim and n - k >= SKIP_MIN_REST:
-                        k = skip(k)
             while k < n and st[0]:
                 step(data[k])
                 k += 1
@@ -235,7 +204,31 @@ class HttpProgram:
                 return self.w[h["ent_tab_off"] + 2 * at + 1]
             at = (at + 1) & h["ent_mask"]
 
+    def slow_ok(self, rid, fvals):
+        """The slow path (regex_vm.h, host build): every slow matcher of rule
+        rid on its field's value; None when an evaluation hit its limits."""
+        h = self.h
+        so, sl = self.w[h["off_slow"] + 2 * rid: h["off_slow"] + 2 * rid + 2]
+        for q in range(sl):
+            f, off = self.w[h["off_pool"] + so + 2 * q], self.w[h["off_pool"] + so + 2 * q + 1]
+            v = fvals.get(f)
+            if v is None:
+                return False
+            r = _VM.vm_host_match(self.prog[off:].ctypes.data, v, len(v), VM_SCRATCH_WORDS, VM_MAX_STEPS)
+            if r < 0:
+                return None
+            if r == 0:
+                return False
+        return True
+
     def eval_record(self, rec: bytes) -> int:
+        """Both passes of the kernel: the first defers a request whose best
+        candidate may be a slow-path rule (kCrSlow), the second
+        (http_slow_kernel) evaluates those rules exactly."""
+        v = self._eval(rec, False)
+        return self._eval(rec, True) if v is None else v
+
+    def _eval(self, rec: bytes, slow: bool):
         h = self.h
         w0, remote, w2, w3, w4 = struct.unpack_from("<5I", rec, 0)
         flags = (w2 >> 16) & 0xFF
@@ -275,8 +268,10 @@ class HttpProgram:
         codes = [0] * h["n_dfas"]
         present = 0
         pos = 20 + 4 * nhdr
+        fvals = {}
 
         def eval_field(f, data):
+            fvals[f] = data
             first, nd, _po, _pl = self.fields[f]
             for k in range(first, first + nd):
                 codes[k] = self.walk(k, data)
@@ -306,6 +301,8 @@ class HttpProgram:
                 pos += nl + vl
         best = h["always_rule"]
         cr = h["off_cr"]
+        min_slow = [KNONE]
+        limit = [KNONE]  # smallest rule whose slow evaluation hit its limits
 
         def remote_ok(rid):
             ro, rl = self.w[h["off_remotes"] + 2 * rid: h["off_remotes"] + 2 * rid + 2]
@@ -327,6 +324,15 @@ class HttpProgram:
                         ok = False
                     elif not (a >> 8) & 1:
                         ok = self.code_has(a >> 9, codes[a >> 9], pat)
+                if ok and hd & CR_SLOW:  # a superset automaton matched
+                    if not slow:
+                        min_slow[0] = min(min_slow[0], rid)
+                        ok = False
+                    else:
+                        r = self.slow_ok(rid, fvals)
+                        if r is None:
+                            limit[0] = min(limit[0], rid)
+                        ok = bool(r)
                 if ok:
                     return rid
                 o += 2 + 2 * nm
@@ -347,6 +353,10 @@ class HttpProgram:
             if (present >> f) & 1:
                 best = scan((self.fields[f][2], self.fields[f][3]), best)
         best = scan((h["zero_off"], h["zero_len"]), best)
+        if not slow and min_slow[0] < best:
+            return None  # deferred to the slow pass
+        if limit[0] < best:  # undecided: a rule before the first match hit the limits
+            return L.VERDICT_UNSUPPORTED
         if best != KNONE:
             return best
         return L.VERDICT_DENY if h0 else L.VERDICT_ALLOW_NO_L7

@@ -98,17 +98,19 @@ def test_invalid_regex_nacks_and_unsupported_is_explicit():
         L.RuleSet.compile_http([L.PortRuleHTTP(Path=ok)])
 
 
-def test_word_boundary_and_lookahead_rules_match_oracle():
-    """Realistic and random rule sets with \\b / \\B / (?=) / (?!) through the
-    program interpreter (the kernel's algorithm) against std::regex_match."""
+def test_word_boundary_lookahead_and_backreference_rules_match_oracle():
+    """Realistic and random rule sets with \\b / \\B / (?=) / (?!) (exact
+    automata) and back-references (superset automata + the slow path, whose
+    executor runs here through its host build) through the program
+    interpreter (the kernel's two passes) against std::regex_match."""
     rng = np.random.default_rng(5)
-    rules = [r for r in X.REALISTIC if "\\1" not in r.Path]
     reqs = X.realistic_requests(rng, 3000) + X.random_requests(rng, 2000)
     arena, offs = L.pack_http(reqs)
-    v = _interp_vs_oracle(rules, arena, offs)
-    assert len(set(v.tolist())) >= 6
-    for trial in range(12):
-        rules = X.random_rules(rng, int(rng.integers(1, 16)))
+    v = _interp_vs_oracle(X.REALISTIC, arena, offs)
+    assert len(set(v.tolist())) >= 8
+    assert {8, 9} <= set(v.tolist())  # the back-reference rules decide some requests
+    for trial in range(16):
+        rules = X.random_rules(rng, int(rng.integers(1, 16)), backrefs=trial % 2 == 1)
         arena, offs = L.pack_http(X.random_requests(rng, 1500))
         _interp_vs_oracle(rules, arena, offs)
 
@@ -227,7 +229,8 @@ def test_regex_compiler_differential_fuzz():
     src = os.path.join(ROOT, "tests", "cpp", "fuzz_regex.cc")
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-o", exe, src,
                            os.path.join(ROOT, "cilium_amd", "csrc", "regex_ecma.cc"),
-                           os.path.join(ROOT, "cilium_amd", "csrc", "dfa_pack.cc")])
+                           os.path.join(ROOT, "cilium_amd", "csrc", "dfa_pack.cc"),
+                           os.path.join(ROOT, "cilium_amd", "csrc", "regex_vm.cc")])
     out = subprocess.run(["timeout", "240", exe, "7", "600", "120"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout[-3000:]
     assert "mismatches=0" in out.stdout

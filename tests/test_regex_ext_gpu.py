@@ -1,0 +1,70 @@
+"""GPU parity of HTTP rules with the ECMAScript constructs beyond the regular
+core that the reference accepts (std::regex via Envoy,
+envoy/cilium_network_policy.h:52-56; verbatim patterns from
+pkg/envoy/server.go:276-289): \\b / \\B and look-ahead (exact automata) and
+back-references (superset automata + the slow pass, http_slow_kernel running
+regex_vm.h), against std::regex_match (oracle/l7oracle.cc), at config-2
+scale and on random rule sets."""
+import numpy as np
+import pytest
+
+import regex_ext_cases as X
+from cilium_amd import l7match as L
+from cilium_amd import workloads as W
+from oracle import HttpOracle
+from program_interp import HttpProgram
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(rules, arena, offs, hits=True):
+    rs = L.RuleSet.compile_http(rules)
+    h = np.zeros(rs.n_counters, dtype=np.uint64) if hits else None
+    got = rs.eval(arena, offs, h)
+    exp = HttpOracle(rules).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+    if hits:
+        assert int(h[0]) == int((exp == -1).sum())
+        for r in np.unique(exp[exp >= 0])[:64]:
+            assert int(h[2 + r]) == int((exp == r).sum())
+        assert int(h.sum()) == len(exp)
+    return got
+
+
+def test_config2_scale_with_extended_rules(gpu):
+    """BASELINE config 2's 1000 rules with the realistic \\b / look-ahead /
+    back-reference rules in front of them (indices 0..9, so they decide
+    first), over 200k config-2 requests plus requests aimed at them."""
+    rng = np.random.default_rng(42)
+    rules = list(X.REALISTIC) + W.rules(2)
+    a1, o1 = W.requests(2, 3_000_000, 200_000)
+    reqs = X.realistic_requests(rng, 20_000) + X.random_requests(rng, 10_000)
+    a2, o2 = L.pack_http(reqs)
+    arena = np.concatenate([a1[:-64], a2])
+    offs = np.concatenate([o1, o2 + np.uint64(len(a1) - 64)])
+    got = _check(rules, arena, offs)
+    assert {0, 1, 2, 8, 9} <= set(got.tolist())
+    assert (got >= len(X.REALISTIC)).sum() > 10_000  # config-2 rules still decide most
+
+
+def test_random_extended_rule_sets(gpu):
+    rng = np.random.default_rng(7)
+    for trial in range(24):
+        rules = X.random_rules(rng, int(rng.integers(1, 24)), backrefs=trial % 2 == 1)
+        arena, offs = L.pack_http(X.random_requests(rng, 4000))
+        _check(rules, arena, offs)
+
+
+def test_slow_path_limits_match_the_host_executor(gpu):
+    """Subjects past the slow path's stack (regex_vm.h kVmScratchWords): the
+    GPU reports L7M_VERDICT_UNSUPPORTED exactly where the host build of the
+    same executor does; short subjects are decided."""
+    rules = [L.PortRuleHTTP(Path="/(a)(?:.)*\\1z"), L.PortRuleHTTP(Path="/.*")]
+    reqs = [L.HTTPRequest("GET", "/a" + "b" * n + "az") for n in (10, 100, 500, 3000, 20000)]
+    arena, offs = L.pack_http(reqs)
+    rs = L.RuleSet.compile_http(rules)
+    got = rs.eval(arena, offs)
+    exp = HttpProgram(rs.program()).eval(arena, offs)
+    assert got.tolist() == exp.tolist()
+    assert got[:2].tolist() == [0, 0] and L.VERDICT_UNSUPPORTED in got.tolist()

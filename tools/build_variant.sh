@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 NAME=$1; FLAGS=${2:-}
 B=cilium_amd/csrc/build_$NAME
 mkdir -p $B variants
-for f in regex_ecma regex_re2 dfa_pack http_compile kafka_compile l7m_api l7m_side l7m_batch; do
+for f in regex_ecma regex_re2 regex_vm dfa_pack http_compile kafka_compile l7m_api l7m_side l7m_batch; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-result $FLAGS -D__HIP_PLATFORM_AMD__ \
     -I/opt/rocm/include -x c++ -c cilium_amd/csrc/$f.cc -o $B/$f.o &
 done
