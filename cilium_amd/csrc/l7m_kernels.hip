@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
 // from HBM, the same walk phase, then verification with the slow-path
 // executor (regex_vm.h) on this lane's scratch.  Verdicts and counters of
 // these requests are written here only.
-constexpr uint32_t kSlowBlocks = 4;  // 4096 lanes x kVmScratchWords words of executor scratch
+constexpr uint32_t kSlowBlocks = 2;  // 2048 lanes x kVmScratchWords words (256 MiB) of executor scratch
 template <int kReg, bool kLit>
 __global__ __launch_bounds__(kBlock) void http_slow_kernel(const uint32_t* __restrict__ prog,
                                                            const uint8_t* __restrict__ arena, uint64_t arena_bytes,

@@ -44,10 +44,12 @@ enum VmOp : uint32_t {
 // header {kind | size << 8, a, b, c} at its top).
 enum VmFrame : uint32_t {
   kFrAltNext = 1,  // a = next, b = cur: after the alternative's left side, try its right side
-  kFrRepNext,      // a = next, b = cur: after "once more" (greedy), leave the loop
+  kFrRepNext,      // a = next | repeat index << 16, b = cur, c = old pos, old count in header bits 16..:
+                   // after "once more" (greedy) restore the counter, then leave the loop
   kFrRepMore,      // a = repeat instruction, b = cur: after leaving (lazy), try once more
   kFrRepRestore,   // a = repeat index, b = pos, c = count
   kFrRepDec,       // a = repeat index
+  kFrRepNextDec,   // a = next | repeat index << 16, b = cur: greedy "once more" at the same position
   kFrCapFirst,     // a = capture, b = old first
   kFrCapEnd,       // a = capture, b = old second, c = old matched
   kFrLook,         // a = next | neg << 31, b = cur, c = begin; payload: snapshot + previous look frame
@@ -56,11 +58,12 @@ enum VmFrame : uint32_t {
 // Result of vm_match.
 constexpr int kVmNoMatch = 0, kVmMatched = 1, kVmLimit = -1;
 // Limits of one evaluation in the HTTP slow pass (and its host restatement in
-// the tests): 32 KiB of state + stack per lane (~2000 frames: libstdc++'s
-// recursion needs one native frame per step of the path and overflows its
-// stack at a few KiB of subject) and 2^22 steps; past either
-// the request's verdict is L7M_VERDICT_UNSUPPORTED.
-constexpr uint32_t kVmScratchWords = 8192;
+// the tests): 128 KiB of state + stack per lane (~8000 four-word frames, one
+// per iteration of a loop over the subject: libstdc++'s recursion needs
+// native frames per step too and overflows its stack at tens of KiB of
+// subject) and 2^22 steps; past either the request's
+// verdict is L7M_VERDICT_UNSUPPORTED.
+constexpr uint32_t kVmScratchWords = 32768;
 constexpr uint32_t kVmMaxSteps = 1u << 22;
 
 __host__ __device__ inline bool vm_is_word(uint32_t c) {
@@ -91,7 +94,7 @@ __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const
   uint32_t i = prog[4];
   auto push4 = [&](uint32_t kind, uint32_t a, uint32_t b, uint32_t c) -> bool {
     if (sp + 4 > cap) return false;
-    st[sp] = kind | 4u << 8;
+    st[sp] = (kind & 0xffu) | 4u << 8 | (kind & ~0xffu);
     st[sp + 1] = a;
     st[sp + 2] = b;
     st[sp + 3] = c;
@@ -122,14 +125,26 @@ __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const
       while (!resumed) {
         if (sp == 0) return kVmNoMatch;
         const uint32_t* h = st + sp - 4;
-        const uint32_t kind = h[0] & 0xffu, size = h[0] >> 8;
+        const uint32_t kind = h[0] & 0xffu, size = kind == kFrLook ? h[0] >> 8 : 4u;
         const uint32_t a = h[1], b = h[2], c = h[3];
         sp -= size;
         switch (kind) {
           case kFrAltNext:
-          case kFrRepNext:
             cur = b;
             i = a;
+            resumed = true;
+            break;
+          case kFrRepNext:  // _M_rep_once_more's restore, then _M_dfs(next)
+            rp[a >> 16] = c;
+            rc[a >> 16] = h[0] >> 16;
+            cur = b;
+            i = a & 0xffffu;
+            resumed = true;
+            break;
+          case kFrRepNextDec:
+            --rc[a >> 16];
+            cur = b;
+            i = a & 0xffffu;
             resumed = true;
             break;
           case kFrRepMore:
@@ -189,9 +204,20 @@ __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const
         i = alt;
         break;
       case kVmRep:
-        if (!ins[4 * i + 3]) {  // greedy
-          ok = push4(kFrRepNext, next, cur, 0);
-          if (ok) i = once_more(i, &ok);
+        if (!ins[4 * i + 3]) {  // greedy: once more (one frame restores the counter and leaves)
+          const uint32_t j = arg;
+          if (rc[j] == 0 || rp[j] != cur) {
+            ok = push4(kFrRepNext | rc[j] << 16, next | j << 16, cur, rp[j]);
+            rp[j] = cur;
+            rc[j] = 1;
+            i = alt;
+          } else if (rc[j] < 2) {
+            ok = push4(kFrRepNextDec, next | j << 16, cur, 0);
+            ++rc[j];
+            i = alt;
+          } else {
+            i = next;
+          }
         } else {
           ok = push4(kFrRepMore, i, cur, 0);
           i = next;

@@ -61,7 +61,7 @@ def test_slow_path_limits_match_the_host_executor(gpu):
     GPU reports L7M_VERDICT_UNSUPPORTED exactly where the host build of the
     same executor does; short subjects are decided."""
     rules = [L.PortRuleHTTP(Path="/(a)(?:.)*\\1z"), L.PortRuleHTTP(Path="/.*")]
-    reqs = [L.HTTPRequest("GET", "/a" + "b" * n + "az") for n in (10, 100, 500, 3000, 20000)]
+    reqs = [L.HTTPRequest("GET", "/a" + "b" * n + "az") for n in (10, 100, 2000, 12000, 40000)]
     arena, offs = L.pack_http(reqs)
     rs = L.RuleSet.compile_http(rules)
     got = rs.eval(arena, offs)
