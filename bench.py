@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--no-batcher", action="store_true", help="skip the per-request batcher leg")
     ap.add_argument("--batcher-seconds", type=float, default=3.0)
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle sample of the timed batch")
+    ap.add_argument("--dialect", choices=["envoy", "re2"], default="envoy",
+                    help="HTTP regex dialect: envoy = std::regex full match (the reference as deployed, default); "
+                         "re2 = Go regexp MatchString (BASELINE.json's wording; RE2 semantics, not run against Go)")
     ap.add_argument("--parity-sample", type=int, default=200_000, help="requests of the timed batch checked")
     return ap.parse_args()
 
@@ -89,7 +92,7 @@ def host_cores():
     return {"affinity": aff, "nproc": os.cpu_count(), "cgroup_quota_cores": quota, "usable": usable}
 
 
-def cpu_baseline(cfg, rules, seconds, threads):
+def cpu_baseline(cfg, rules, seconds, threads, dialect=L.DIALECT_ENVOY_ECMA_FULL):
     """Oracle (the reference algorithm restated: per-request linear rule scan,
     std::regex_match per matcher; K4 coverage for Kafka) timed on the host on a
     bounded sample, on `threads` threads (all the host cores this process may
@@ -103,7 +106,8 @@ def cpu_baseline(cfg, rules, seconds, threads):
     engine = "nfa" if cfg == 5 else "std"
     # the reference's per-request loop as Envoy runs it: every rule's matchers,
     # no prefilter (parity_leg uses the prefiltered scan)
-    orc = HttpOracle(rules, engine=engine, prefilter=False) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+    orc = (HttpOracle(rules, dialect=dialect, engine=engine, prefilter=False) if proto == L.PROTO_HTTP
+           else KafkaOracle(rules))
     n0 = 20_000 if cfg != 5 else 16 * threads
 
     def sample(start, n):
@@ -127,7 +131,9 @@ def cpu_baseline(cfg, rules, seconds, threads):
     dt1 = time.perf_counter() - t
     hc = host_cores()
     what = ("oracle/l7oracle.cc with the NFA engine (oracle/nfa.h; linear rule scan, Pike-VM full match)"
-            if engine == "nfa" else "oracle/l7oracle.cc (std::regex_match linear rule scan)"
+            if engine == "nfa" else ("oracle/l7oracle.cc (std::regex_search linear rule scan, RE2 dialect)"
+                                     if dialect == L.DIALECT_RE2_SEARCH else
+                                     "oracle/l7oracle.cc (std::regex_match linear rule scan)")
             if proto == L.PROTO_HTTP else "oracle/l7oracle.cc (ReadRequest + MatchesRule)")
     return {"value": len(o) / dt, "unit": "verdicts/s", "cores": threads, "kind": "port",
             "single_thread_value": len(o1) / dt1, "cpu_model": cpu_model(), "host": hc,
@@ -137,7 +143,8 @@ def cpu_baseline(cfg, rules, seconds, threads):
                       f"single_thread_value: the first {len(o1)} of them on 1 thread, {dt1:.1f} s"}
 
 
-def parity_leg(cfg, rules, verdicts, lo, n, threads, n_sample=200_000, blocks=256, seed=None, n_rules=None):
+def parity_leg(cfg, rules, verdicts, lo, n, threads, n_sample=200_000, blocks=256, seed=None, n_rules=None,
+               dialect=L.DIALECT_ENVOY_ECMA_FULL):
     """The timed batch's own verdicts against the oracle (test infrastructure,
     outside the timed region): `blocks` contiguous runs of requests spread
     evenly over this rank's shard [lo, lo + n), n_sample requests in all (the
@@ -150,7 +157,7 @@ def parity_leg(cfg, rules, verdicts, lo, n, threads, n_sample=200_000, blocks=25
     proto = W.CONFIGS[gcfg]["proto"]
     engine = "nfa" if cfg == 5 else "std"
     t0 = time.perf_counter()
-    orc = HttpOracle(rules, engine=engine) if proto == L.PROTO_HTTP else KafkaOracle(rules)
+    orc = HttpOracle(rules, dialect=dialect, engine=engine) if proto == L.PROTO_HTTP else KafkaOracle(rules)
     if n <= n_sample:
         runs = [(0, n)]
     else:
@@ -269,8 +276,11 @@ def main():
     n_job = (args.requests or c["n_requests"]) * (world if scaling == "weak" else 1)
 
     rules = W.rules(cfg)
-    rs = (L.RuleSet.compile_http(rules, lds_budget_bytes=args.lds_budget) if c["proto"] == L.PROTO_HTTP
-          else L.RuleSet.compile_kafka(rules))
+    dialect = L.DIALECT_RE2_SEARCH if args.dialect == "re2" else L.DIALECT_ENVOY_ECMA_FULL
+    if dialect != L.DIALECT_ENVOY_ECMA_FULL and c["proto"] != L.PROTO_HTTP:
+        raise SystemExit("--dialect applies to HTTP configurations")
+    rs = (L.RuleSet.compile_http(rules, dialect=dialect, lds_budget_bytes=args.lds_budget)
+          if c["proto"] == L.PROTO_HTTP else L.RuleSet.compile_kafka(rules))
 
     # ---- rank's byte-balanced shard, generated deterministically, in HBM ----
     lo, hi = D.balanced_shard(cfg, n_job, world, rank, threads=threads,
@@ -348,7 +358,9 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": METRIC if cfg == 2 else f"L7 verdicts/sec ({c['name']}) + achieved HBM GB/s vs peak",
+            "metric": (METRIC if cfg == 2 and dialect == L.DIALECT_ENVOY_ECMA_FULL else
+                       f"L7 verdicts/sec ({c['name']}{', RE2 MatchString dialect' if dialect else ''}) + achieved "
+                       f"HBM GB/s vs peak"),
             "value": value,
             "unit": "verdicts/s",
             "n_gpus": world,
@@ -360,7 +372,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic generator libl7gen.so, SURVEY.md §8(d))",
-            "config": {"workload": c["name"], "baseline_config": cfg, "n_rules": len(rules),
+            "config": {"workload": c["name"] + ("-re2" if dialect else ""), "baseline_config": cfg,
+                       "dialect": ("re2-search (Go regexp MatchString semantics; RE2 semantics, not run against Go)"
+                                   if dialect else "envoy-ecma-full (std::regex_match, the reference as deployed)"),
+                       "n_rules": len(rules),
                        "requests_per_gpu": per_gpu, "requests_total": n_job, "seed": hex(c["seed"]),
                        "mean_record_bytes": rec_bytes / per_gpu,
                        "parallelism": f"dp{world} (byte-balanced request shards, "
@@ -369,7 +384,7 @@ def main():
                        "dfa_groups": int(rs.info.n_dfas), "dfa_states": int(rs.info.total_dfa_states)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
-                         "traffic": measured_traffic(cfg) if not args.requests else None,
+                         "traffic": measured_traffic(cfg) if not args.requests and not dialect else None,
                          "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_launch": alg_bytes},
             "counters_ok": hits_total == expect_hits,
             "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
@@ -378,19 +393,20 @@ def main():
         if not args.no_parity and not args.diag:
             log("parity sample (oracle, outside the timed region)")
             res["parity"] = parity_leg(cfg, rules, d_verd.cpu().numpy(), lo, per_gpu,
-                                       args.threads or host_cores()["usable"], n_sample=args.parity_sample)
+                                       args.threads or host_cores()["usable"], n_sample=args.parity_sample,
+                                       dialect=dialect)
             log(f"parity: {res['parity']['mismatches']} mismatches in {res['parity']['sampled']}")
         if keep_host:
             log("end-to-end (pinned host arena)")
             res["e2e"] = e2e_leg(rs, pinned.numpy(), host_offs, per_gpu)
             del pinned
-        if world == 1 and not args.no_batcher and not args.diag and cfg in (2, 3) and not args.requests:
+        if world == 1 and not args.no_batcher and not args.diag and cfg in (2, 3) and not args.requests and not dialect:
             log("batcher (per-request calls)")
             res["batcher"] = batcher_leg(cfg, args.batcher_seconds)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds,
-                                               args.threads or host_cores()["usable"])
+                                               args.threads or host_cores()["usable"], dialect=dialect)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
