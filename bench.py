@@ -204,13 +204,18 @@ def e2e_leg(rs, arena_pinned, offs, n, passes=2):
 
 def batcher_leg(cfg, seconds):
     """Per-request blocking calls through l7m_batcher (cilium_amd/batcher_bench,
-    a plain C client): verdicts/s and latency at 8 / 64 / 512 caller threads,
-    deadline batching (max_delay 200 us) and eager batching."""
+    a plain C client): verdicts/s, latency percentiles and the per-batch
+    phases (fill / launch / gpu / wake) at 8 caller threads and at one per
+    usable core (more callers than cores measure the cgroup's CPU quota, not
+    the batcher: each line reports the cgroup's throttling during its run),
+    eager batching and deadline batching (max_delay 200 us)."""
     import subprocess
     exe = os.path.join(ROOT, "cilium_amd", "batcher_bench")
+    usable = host_cores()["usable"]
+    counts = sorted({8, max(8, usable)})
     out = []
     for eager in (1, 0):
-        p = subprocess.run([exe, str(cfg), "1000000", str(seconds), str(eager), "8", "64", "512"],
+        p = subprocess.run([exe, str(cfg), "1000000", str(seconds), str(eager)] + [str(c) for c in counts],
                            capture_output=True, text=True, timeout=120)
         if p.returncode != 0:
             return {"error": p.stderr[-500:]}

@@ -64,6 +64,20 @@ static void* worker(void* p) {
   return NULL;
 }
 
+/* cgroup v2 CPU throttling counters (/sys/fs/cgroup/cpu.stat), -1 if absent */
+static void cpu_stat(long long* nr_throttled, long long* throttled_usec) {
+  *nr_throttled = *throttled_usec = -1;
+  FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return;
+  char k[64];
+  long long v;
+  while (fscanf(f, "%63s %lld", k, &v) == 2) {
+    if (!strcmp(k, "nr_throttled")) *nr_throttled = v;
+    if (!strcmp(k, "throttled_usec")) *throttled_usec = v;
+  }
+  fclose(f);
+}
+
 static int cmpf(const void* x, const void* y) {
   const float a = *(const float*)x, b = *(const float*)y;
   return a < b ? -1 : a > b;
@@ -171,6 +185,8 @@ int main(int argc, char** argv) {
     const uint64_t cap = 4000000 / T + 1000;
     uint64_t b0 = 0, r0 = 0;
     l7m_batcher_stats(g_b, &b0, &r0);
+    long long thr0, thu0, thr1, thu1;
+    cpu_stat(&thr0, &thu0);
     const double t0 = now_s();
     g_end = t0 + secs;
     for (int t = 0; t < T; ++t) {
@@ -186,8 +202,12 @@ int main(int argc, char** argv) {
       bad += args[t].bad;
     }
     const double dt = now_s() - t0;
+    cpu_stat(&thr1, &thu1);
     uint64_t b1 = 0, r1 = 0;
     l7m_batcher_stats(g_b, &b1, &r1);
+    l7m_batcher_profile pf;
+    memset(&pf, 0, sizeof pf);
+    l7m_batcher_get_profile(g_b, &pf);
     float* all = malloc((done ? done : 1) * sizeof(float));
     uint64_t k = 0;
     for (int t = 0; t < T; ++t) {
@@ -197,11 +217,14 @@ int main(int argc, char** argv) {
     }
     qsort(all, done, sizeof(float), cmpf);
     printf("{\"threads\": %d, \"eager\": %d, \"verdicts_per_s\": %.1f, \"p50_us\": %.1f, \"p99_us\": %.1f, "
-           "\"max_us\": %.1f, \"batches\": %llu, \"mean_batch\": %.1f, \"requests\": %llu, \"mismatches\": %llu}\n",
+           "\"max_us\": %.1f, \"batches\": %llu, \"mean_batch\": %.1f, \"requests\": %llu, \"mismatches\": %llu, "
+           "\"phases_us\": {\"fill\": %.2f, \"launch\": %.2f, \"gpu\": %.2f, \"wake\": %.2f}, "
+           "\"cgroup_nr_throttled\": %lld, \"cgroup_throttled_usec\": %lld}\n",
            T, eager, done / dt, done ? all[done / 2] : 0.0, done ? all[(uint64_t)(done * 0.99)] : 0.0,
            done ? all[done - 1] : 0.0, (unsigned long long)(b1 - b0),
            (b1 - b0) ? (double)(r1 - r0) / (double)(b1 - b0) : 0.0, (unsigned long long)done,
-           (unsigned long long)bad);
+           (unsigned long long)bad, pf.fill_us, pf.launch_us, pf.gpu_us, pf.wake_us,
+           thr0 >= 0 ? thr1 - thr0 : -1, thu0 >= 0 ? thu1 - thu0 : -1);
     fflush(stdout);
     free(all);
     free(args);

@@ -7,26 +7,34 @@
 // NetworkPolicyMap::Allowed (envoy/cilium_l7policy.cc:126-186).  A GPU call
 // per request would cost more than the verdict, so the batcher keeps that
 // per-request, blocking call shape while many callers' requests share one
-// l7m_eval: a caller appends its record to the batch being filled and waits;
-// a flusher evaluates the batch when it holds max_batch requests or its first
-// request has waited max_delay_us, while the next batch fills.
+// evaluation: a caller appends its record to the batch being filled and
+// waits; a flusher evaluates the batch (eagerly, as soon as it is free, or
+// when max_batch are pending / the first has waited max_delay_us) while the
+// next batch fills.
 //
-// Pipelining: `in_flight` flusher threads (default 2) each take the next
-// ready batch (with `eager`, as soon as a flusher is free: batches then grow
-// with the load instead of waiting for max_delay_us), so batch k+1's H2D copy runs while batch k's kernel and D2H
-// run (l7m_eval is reentrant: every call has its own stream and device
-// buffers).  Batches live in pinned host memory (recycled, never freed while
-// the batcher lives), so the copies are DMA transfers, not staged.
+// Latency path (round 4):
+//   * append without a lock: a caller reserves its slot and its arena bytes
+//     with one compare-and-swap on the batch's reservation word (count,
+//     bytes, closed bit), copies its record and bumps `written`;
+//   * batches are preallocated pinned, device-mapped host buffers (arena,
+//     offsets, identities, verdicts): the kernels read the records and write
+//     the verdicts in place over PCIe (l7m_eval_device on the mapped
+//     pointers), no staging copies;
+//   * a flusher closes the batch (sets the closed bit, installs a fresh
+//     batch), waits for the reserved slots to be written, enqueues the
+//     kernels on its own stream and polls an event for completion;
+//   * callers spin briefly on the batch's done flag, then sleep on its
+//     condition variable.
+// l7m_batcher_get_profile breaks the per-batch time into these phases.
 // l7m_batcher_set_ruleset is the policy update (Redirect.updateRules,
 // pkg/proxy/redirect.go:68-74): batches flushed afterwards use the new rules.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <chrono>
-#include <cstddef>
 #include <condition_variable>
+#include <cstddef>
 #include <cstring>
-#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -36,164 +44,318 @@
 namespace {
 
 using Clock = std::chrono::steady_clock;
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
 
-// Growable pinned host buffer (hipHostMalloc); grows by doubling.
-template <class T>
-struct PinnedVec {
-  T* p = nullptr;
-  size_t n = 0, cap = 0;
-  PinnedVec() = default;
-  PinnedVec(const PinnedVec&) = delete;
-  PinnedVec& operator=(const PinnedVec&) = delete;
-  ~PinnedVec() {
-    if (p) (void)hipHostFree(p);
-  }
-  bool reserve(size_t want) {
-    if (want <= cap) return true;
-    size_t c = cap ? cap : 1024;
-    while (c < want) c *= 2;
-    void* q = nullptr;
-    if (hipHostMalloc(&q, c * sizeof(T), hipHostMallocDefault) != hipSuccess) return false;
-    if (n) std::memcpy(q, p, n * sizeof(T));
-    if (p) (void)hipHostFree(p);
-    p = static_cast<T*>(q);
-    cap = c;
+// Reservation word of a batch: closed bit | record count << 40 | arena bytes.
+constexpr uint64_t kClosed = 1ull << 63;
+constexpr int kCountShift = 40;
+constexpr uint64_t kBytesMask = (1ull << kCountShift) - 1;
+constexpr uint32_t count_of(uint64_t s) { return static_cast<uint32_t>((s & ~kClosed) >> kCountShift); }
+constexpr uint64_t bytes_of(uint64_t s) { return s & kBytesMask; }
+constexpr int64_t kSpinNs = 50000;  // a caller spins this long for its verdict, then sleeps
+
+struct Batch {
+  // one pinned, device-mapped allocation: arena (arena_cap + 64 bytes of
+  // readable slack) | offsets | identities | verdicts
+  void* host = nullptr;
+  uint8_t* arena = nullptr;
+  uint64_t* offs = nullptr;
+  uint32_t* ids = nullptr;
+  int32_t* verd = nullptr;
+  const void *d_arena = nullptr, *d_offs = nullptr, *d_ids = nullptr;
+  void* d_verd = nullptr;
+  size_t arena_cap = 0;
+  uint32_t cap = 0;
+  std::atomic<uint64_t> resv{0};
+  std::atomic<uint32_t> written{0};  // reserved slots whose record is in place
+  std::atomic<uint32_t> done{0};
+  std::atomic<uint32_t> readers{0};  // callers that have not read their verdict yet
+  std::atomic<uint32_t> sleepers{0};
+  std::atomic<uint32_t> want_close{0};  // a caller found no room
+  std::atomic<int64_t> first_ns{0};
+  int64_t done_ns = 0;
+  int rc = L7M_OK;
+  std::mutex m;
+  std::condition_variable cv;
+
+  bool alloc(size_t acap, uint32_t rcap) {
+    const size_t a = (acap + 64 + 255) & ~size_t(255);
+    const size_t o = (static_cast<size_t>(rcap) * 8 + 255) & ~size_t(255);
+    const size_t i = (static_cast<size_t>(rcap) * 4 + 255) & ~size_t(255);
+    const size_t v = static_cast<size_t>(rcap) * 4;
+    if (hipHostMalloc(&host, a + o + i + v, hipHostMallocMapped) != hipSuccess) {
+      host = nullptr;
+      return false;
+    }
+    uint8_t* p = static_cast<uint8_t*>(host);
+    arena = p;
+    offs = reinterpret_cast<uint64_t*>(p + a);
+    ids = reinterpret_cast<uint32_t*>(p + a + o);
+    verd = reinterpret_cast<int32_t*>(p + a + o + i);
+    std::memset(arena, 0, a);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess || !d) return false;
+    uint8_t* dp = static_cast<uint8_t*>(d);
+    d_arena = dp;
+    d_offs = dp + a;
+    d_ids = dp + a + o;
+    d_verd = dp + a + o + i;
+    arena_cap = acap;
+    cap = rcap;
     return true;
   }
-};
-
-// A batch's completion has its own mutex / condition variable, so finishing
-// one batch wakes only its callers (no thundering herd across batches) and
-// they do not contend with callers appending to the next batch.
-struct Batch {
-  PinnedVec<uint8_t> arena;
-  PinnedVec<uint64_t> offs;
-  PinnedVec<uint32_t> ids;  // source identities (Kafka rule sets)
-  PinnedVec<int32_t> verd;
-  Clock::time_point first;
-  std::mutex m;             // guards done, rc, waiters
-  std::condition_variable cv;
-  bool done = false;
-  int rc = L7M_OK;
-  uint32_t waiters = 0;  // callers that have not read their verdict yet
+  ~Batch() {
+    if (host) (void)hipHostFree(host);
+  }
   void reset() {
-    arena.n = offs.n = ids.n = verd.n = 0;
-    done = false;
+    resv.store(0);
+    written.store(0);
+    done.store(0);
+    readers.store(0);
+    sleepers.store(0);
+    want_close.store(0);
+    first_ns.store(0);
     rc = L7M_OK;
-    waiters = 0;
   }
 };
 
 }  // namespace
 
 struct l7m_batcher {
-  std::mutex mu;  // guards cur, pool, rs, stop, stats (lock order: mu, then a batch's m)
-  std::condition_variable cv_flush, cv_idle;
-  l7m_ruleset* rs = nullptr;
   uint32_t max_batch = 65536;
   uint32_t max_delay_us = 200;
   uint32_t in_flight = 2;
-  bool eager = false;  // flush as soon as a flusher is free (no deadline wait)
+  bool eager = false;
   int device = 0;
-  Batch* cur = nullptr;
-  std::vector<Batch*> pool;     // recycled batches (pinned buffers kept)
-  std::vector<Batch*> all;      // every batch ever made (freed at destroy)
-  bool stop = false;
-  std::atomic<uint32_t> callers{0};  // threads inside eval()
-  uint64_t batches = 0, requests = 0;
+  size_t arena_cap = 16u << 20;
+  std::atomic<Batch*> cur{nullptr};
+  std::mutex rs_mu;  // guards rs
+  l7m_ruleset* rs = nullptr;
+  std::mutex close_mu;  // flushers: close a batch + install the next
+  std::mutex pool_mu;   // guards pool, all
+  std::vector<Batch*> pool, all;
+  std::atomic<bool> stop{false};
+  std::atomic<uint32_t> callers{0};
+  std::atomic<uint32_t> idle{0};  // flushers asleep
+  std::mutex idle_mu;
+  std::condition_variable idle_cv;
   std::vector<std::thread> flushers;
+  // statistics (l7m_batcher_stats / l7m_batcher_get_profile)
+  std::atomic<uint64_t> batches{0}, requests{0}, fill_ns{0}, launch_ns{0}, gpu_ns{0}, wake_ns{0};
 
-  Batch* fresh() {  // under mu
-    Batch* b;
-    if (!pool.empty()) {
-      b = pool.back();
-      pool.pop_back();
-    } else {
-      b = new Batch();
-      all.push_back(b);
+  Batch* fresh() {
+    {
+      std::lock_guard<std::mutex> g(pool_mu);
+      if (!pool.empty()) {
+        Batch* b = pool.back();
+        pool.pop_back();
+        b->reset();
+        return b;
+      }
     }
-    b->reset();
+    auto* b = new (std::nothrow) Batch();
+    if (!b) return nullptr;
+    (void)hipSetDevice(device);
+    if (!b->alloc(arena_cap, max_batch)) {
+      delete b;
+      return nullptr;
+    }
+    std::lock_guard<std::mutex> g(pool_mu);
+    all.push_back(b);
     return b;
+  }
+  void recycle(Batch* b) {
+    std::lock_guard<std::mutex> g(pool_mu);
+    pool.push_back(b);
+  }
+  void wake_flusher() {
+    if (idle.load() == 0) return;
+    std::lock_guard<std::mutex> g(idle_mu);
+    idle_cv.notify_one();
   }
 
   void run() {
     (void)hipSetDevice(device);
-    std::unique_lock<std::mutex> lk(mu);
+    hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;
+    const bool dev_ok = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
+                        hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
     for (;;) {
-      while (!stop && cur->offs.n == 0) cv_flush.wait(lk);
-      if (cur->offs.n == 0 && stop) return;
-      // full, or the first request has waited long enough (or shutting down)
-      Batch* const b = cur;
-      const auto deadline = b->first + std::chrono::microseconds(max_delay_us);
-      while (!eager && !stop && cur == b && b->offs.n < max_batch && Clock::now() < deadline)
-        cv_flush.wait_until(lk, deadline);
-      if (cur != b) continue;  // another flusher took it
-      cur = fresh();
-      l7m_ruleset* r = rs;
-      l7m_retain(r);
-      ++batches;
-      requests += b->offs.n;
-      lk.unlock();
-      cv_flush.notify_one();  // a second flusher may start on the next batch
-      int rc = b->verd.reserve(b->offs.n) ? L7M_OK : L7M_ENOMEM;
-      if (rc == L7M_OK) {
-        l7m_ruleset_info info;
-        l7m_ruleset_get_info(r, &info);
-        rc = l7m_eval_ids(r, b->arena.p, b->arena.n, b->offs.p, b->offs.n,
-                          info.proto == L7M_PROTO_KAFKA ? b->ids.p : nullptr, b->verd.p, nullptr, 0);
+      Batch* b = cur.load(std::memory_order_acquire);
+      const uint64_t s0 = b->resv.load(std::memory_order_acquire);
+      const uint32_t cnt0 = count_of(s0);
+      if (cnt0 == 0) {
+        if (stop.load()) break;
+        // idle: poll a little, then sleep until a caller's first append
+        const int64_t t0 = now_ns();
+        bool work = false;
+        while (now_ns() - t0 < 20000) {
+          if (count_of(cur.load(std::memory_order_acquire)->resv.load(std::memory_order_acquire)) || stop.load()) {
+            work = true;
+            break;
+          }
+          cpu_relax();
+        }
+        if (!work) {
+          std::unique_lock<std::mutex> lk(idle_mu);
+          idle.fetch_add(1);
+          if (!count_of(cur.load()->resv.load()) && !stop.load())
+            idle_cv.wait_for(lk, std::chrono::milliseconds(2));
+          idle.fetch_sub(1);
+        }
+        continue;
       }
-      l7m_release(r);
+      if (!eager && !stop.load() && cnt0 < max_batch && !b->want_close.load() &&
+          now_ns() - b->first_ns.load() < static_cast<int64_t>(max_delay_us) * 1000) {
+        cpu_relax();
+        continue;
+      }
+      uint64_t s;
       {
-        std::lock_guard<std::mutex> g(b->m);
-        b->rc = rc;
-        b->done = true;
+        std::lock_guard<std::mutex> g(close_mu);
+        if (cur.load() != b) continue;  // another flusher took it
+        Batch* nb = fresh();
+        if (!nb) {  // out of pinned memory: evaluate what is there, keep filling b's successor later
+          std::this_thread::sleep_for(std::chrono::microseconds(100));
+          continue;
+        }
+        s = b->resv.fetch_or(kClosed);
+        cur.store(nb, std::memory_order_release);
       }
-      b->cv.notify_all();
-      lk.lock();
+      const uint32_t cnt = count_of(s);
+      const uint64_t bytes = bytes_of(s);
+      const int64_t t_close = now_ns();
+      while (b->written.load(std::memory_order_acquire) < cnt) cpu_relax();
+      l7m_ruleset* r;
+      {
+        std::lock_guard<std::mutex> g(rs_mu);
+        r = rs;
+        l7m_retain(r);
+      }
+      l7m_ruleset_info info;
+      l7m_ruleset_get_info(r, &info);
+      int rc = dev_ok ? L7M_OK : L7M_EDEVICE;
+      if (rc == L7M_OK)
+        rc = l7m_eval_device_ids(r, b->d_arena, bytes, b->d_offs, cnt,
+                                 info.proto == L7M_PROTO_KAFKA ? b->d_ids : nullptr, b->d_verd, nullptr, stream, 0);
+      const int64_t t_launch = now_ns();
+      if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
+      if (rc == L7M_OK) {
+        hipError_t q;
+        while ((q = hipEventQuery(ev)) == hipErrorNotReady) cpu_relax();
+        if (q != hipSuccess) rc = L7M_EDEVICE;
+      }
+      const int64_t t_done = now_ns();
+      l7m_release(r);
+      batches.fetch_add(1);
+      requests.fetch_add(cnt);
+      fill_ns.fetch_add(static_cast<uint64_t>(t_close - b->first_ns.load()));
+      launch_ns.fetch_add(static_cast<uint64_t>(t_launch - t_close));
+      gpu_ns.fetch_add(static_cast<uint64_t>(t_done - t_launch));
+      b->rc = rc;
+      b->done_ns = t_done;
+      b->readers.store(cnt);
+      b->done.store(1);  // seq_cst with the callers' sleepers increment (no lost wake-up)
+      if (b->sleepers.load()) {
+        std::lock_guard<std::mutex> g(b->m);
+        b->cv.notify_all();
+      }
     }
+    if (ev) (void)hipEventDestroy(ev);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  // A record that can never fit a batch: evaluated alone (copying path).
+  int eval_alone(const uint8_t* rec, size_t len, uint32_t src_identity, int32_t* verdict) {
+    l7m_ruleset* r;
+    {
+      std::lock_guard<std::mutex> g(rs_mu);
+      r = rs;
+      l7m_retain(r);
+    }
+    std::vector<uint8_t> a((len + 3 + 64) & ~size_t(3), 0);
+    if (len) std::memcpy(a.data(), rec, len);
+    const uint64_t off = 0;
+    (void)hipSetDevice(device);
+    l7m_ruleset_info info;
+    l7m_ruleset_get_info(r, &info);
+    const int rc = l7m_eval_ids(r, a.data(), (len + 3) & ~size_t(3), &off, 1,
+                                info.proto == L7M_PROTO_KAFKA ? &src_identity : nullptr, verdict, nullptr, 0);
+    l7m_release(r);
+    return rc;
   }
 
   int eval(const uint8_t* rec, size_t len, uint32_t src_identity, int32_t* verdict) {
-    std::unique_lock<std::mutex> lk(mu);
-    if (stop) return L7M_EINVAL;
-    Batch* b = cur;
-    const size_t idx = b->offs.n;
-    const size_t off = b->arena.n, padded = (len + 3) & ~size_t(3);
-    // + 64 bytes of zero tail for the kernels' aligned loads (l7m_eval pads its copy too)
-    if (!b->arena.reserve(off + padded + 64) || !b->offs.reserve(idx + 1) || !b->ids.reserve(idx + 1))
-      return L7M_ENOMEM;
+    if (stop.load()) return L7M_EINVAL;
     callers.fetch_add(1);
-    if (idx == 0) b->first = Clock::now();
-    b->offs.p[idx] = off;
-    b->ids.p[idx] = src_identity;
-    if (len) std::memcpy(b->arena.p + off, rec, len);
-    std::memset(b->arena.p + off + len, 0, padded - len);
-    b->arena.n = off + padded;
-    b->offs.n = idx + 1;
-    {
-      std::lock_guard<std::mutex> g(b->m);  // b is not in flight yet: done is false
-      ++b->waiters;
+    if (stop.load()) {
+      callers.fetch_sub(1);
+      return L7M_EINVAL;
     }
-    if (idx == 0 || b->offs.n >= max_batch) cv_flush.notify_one();
-    lk.unlock();
-    int rc;
-    bool last;
-    {
-      std::unique_lock<std::mutex> bl(b->m);
-      b->cv.wait(bl, [&] { return b->done; });
-      rc = b->rc;
-      if (rc == L7M_OK) *verdict = b->verd.p[idx];
-      last = --b->waiters == 0;
+    const size_t padded = (len + 3) & ~size_t(3);
+    if (padded > arena_cap) {
+      const int rc = eval_alone(rec, len, src_identity, verdict);
+      callers.fetch_sub(1);
+      return rc;
     }
-    if (last) {  // the last reader recycles the batch
-      lk.lock();
-      pool.push_back(b);
-      lk.unlock();
+    // reserve a slot and its bytes in the batch being filled
+    Batch* b;
+    uint32_t idx;
+    uint64_t off;
+    for (;;) {
+      b = cur.load(std::memory_order_acquire);
+      uint64_t s = b->resv.load(std::memory_order_acquire);
+      if (s & kClosed) {
+        cpu_relax();
+        continue;
+      }
+      const uint32_t cnt = count_of(s);
+      if (cnt >= b->cap || bytes_of(s) + padded > b->arena_cap) {  // full: the flusher takes it
+        b->want_close.store(1);
+        wake_flusher();
+        cpu_relax();
+        continue;
+      }
+      if (b->resv.compare_exchange_weak(s, s + (1ull << kCountShift) + padded, std::memory_order_acq_rel)) {
+        idx = cnt;
+        off = bytes_of(s);
+        break;
+      }
     }
-    if (callers.fetch_sub(1) == 1) {
-      std::lock_guard<std::mutex> g(mu);
-      cv_idle.notify_all();
+    if (idx == 0) b->first_ns.store(now_ns());
+    if (len) std::memcpy(b->arena + off, rec, len);
+    if (padded != len) std::memset(b->arena + off + len, 0, padded - len);
+    b->offs[idx] = off;
+    b->ids[idx] = src_identity;
+    b->written.fetch_add(1, std::memory_order_release);
+    if (idx == 0 || idx + 1 >= max_batch) wake_flusher();
+    // wait for the verdict: spin, then sleep
+    const int64_t t0 = now_ns();
+    uint32_t spins = 0;
+    while (!b->done.load(std::memory_order_acquire)) {
+      if ((++spins & 63) == 0 && now_ns() - t0 > kSpinNs) {
+        b->sleepers.fetch_add(1);
+        std::unique_lock<std::mutex> lk(b->m);
+        b->cv.wait(lk, [&] { return b->done.load() != 0; });
+        b->sleepers.fetch_sub(1);
+        break;
+      }
+      cpu_relax();
     }
+    const int rc = b->rc;
+    if (rc == L7M_OK) *verdict = b->verd[idx];
+    wake_ns.fetch_add(static_cast<uint64_t>(now_ns() - b->done_ns));
+    if (b->readers.fetch_sub(1) == 1) recycle(b);  // the last reader recycles the batch
+    callers.fetch_sub(1);
     return rc;
   }
 };
@@ -215,7 +377,15 @@ int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batche
     if (k >= offsetof(l7m_batcher_opts, eager) + sizeof o.eager) b->eager = o.eager != 0;
     b->device = o.device;
   }
-  b->cur = b->fresh();
+  // arena of a batch: about 256 bytes per request, 1-16 MiB
+  const size_t want = static_cast<size_t>(b->max_batch) * 256u;
+  b->arena_cap = want < (1u << 20) ? (1u << 20) : want > (16u << 20) ? (16u << 20) : want;
+  Batch* first = b->fresh();
+  if (!first) {
+    delete b;
+    return L7M_ENOMEM;
+  }
+  b->cur.store(first);
   l7m_retain(rs);
   b->rs = rs;
   for (uint32_t i = 0; i < b->in_flight; ++i) b->flushers.emplace_back([b] { b->run(); });
@@ -228,7 +398,7 @@ int l7m_batcher_set_ruleset(l7m_batcher* b, l7m_ruleset* rs) {
   l7m_retain(rs);
   l7m_ruleset* old;
   {
-    std::lock_guard<std::mutex> lk(b->mu);
+    std::lock_guard<std::mutex> lk(b->rs_mu);
     old = b->rs;
     b->rs = rs;
   }
@@ -258,9 +428,20 @@ int l7m_batcher_eval_http(l7m_batcher* b, const l7m_http_request* req, int32_t* 
 
 int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests) {
   if (!b) return L7M_EINVAL;
-  std::lock_guard<std::mutex> lk(b->mu);
-  if (batches) *batches = b->batches;
-  if (requests) *requests = b->requests;
+  if (batches) *batches = b->batches.load();
+  if (requests) *requests = b->requests.load();
+  return L7M_OK;
+}
+
+int l7m_batcher_get_profile(l7m_batcher* b, l7m_batcher_profile* out) {
+  if (!b || !out) return L7M_EINVAL;
+  const uint64_t nb = b->batches.load(), nr = b->requests.load();
+  out->batches = nb;
+  out->requests = nr;
+  out->fill_us = nb ? b->fill_ns.load() / 1e3 / nb : 0.0;
+  out->launch_us = nb ? b->launch_ns.load() / 1e3 / nb : 0.0;
+  out->gpu_us = nb ? b->gpu_ns.load() / 1e3 / nb : 0.0;
+  out->wake_us = nr ? b->wake_ns.load() / 1e3 / nr : 0.0;
   return L7M_OK;
 }
 
@@ -269,17 +450,16 @@ int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests) {
 // l7m_batcher_eval* has read its verdict and left.
 void l7m_batcher_destroy(l7m_batcher* b) {
   if (!b) return;
+  b->stop.store(true);
   {
-    std::lock_guard<std::mutex> lk(b->mu);
-    b->stop = true;
+    std::lock_guard<std::mutex> g(b->idle_mu);
+    b->idle_cv.notify_all();
   }
-  b->cv_flush.notify_all();
+  // callers already inside finish their reservation; flushers drain the
+  // pending batches and exit once the current batch stays empty
+  while (b->callers.load() != 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
   for (auto& t : b->flushers)
     if (t.joinable()) t.join();
-  {
-    std::unique_lock<std::mutex> lk(b->mu);
-    b->cv_idle.wait(lk, [&] { return b->callers.load() == 0; });
-  }
   l7m_release(b->rs);
   for (Batch* x : b->all) delete x;
   delete b;

@@ -366,41 +366,25 @@ __device__ __forceinline__ uint32_t topic_first(const KView& v, const uint8_t* t
   return probe_topic(v, v.slots[nm.hash & (v.n_slots - 1)], nm.hash, nm, t, tlen, kok, kind, version, client, gmask);
 }
 
-// Topics are resolved after the decode, by all lanes of the wave together
-// (the decode itself diverges by request kind): each lane parks the stage
-// offsets of its first kTopicQ topic names in its LDS column; after the
-// tile's decode the parked names of all 64 requests are compacted into one
-// list and spread over the lanes (lane l takes entries l, l + 64, ...), so a
-// tile with T parked topics costs ceil(T / 64) lookup rounds (config 3: ~2.5
-// topics per request, 3 rounds) instead of the largest per-request count (4),
-// with every lane busy.  Because MatchesRule's result is
+// Topics are resolved after the decode, all lanes of the wave together
+// (the decode itself diverges by request kind): each lane parks the offsets
+// of its first kTopicQ topic names in its LDS column and the lookups run in
+// lock-step rounds.  Because MatchesRule's result is
 //   min(j, max over topics of f(t))   (f(t) = topic_first, kNone = uncovered)
 // with j the first Topic=="" rule, the per-topic terms need neither j nor
-// any order: each is folded into its request's maximum with an LDS atomic
-// max, and a request with more topics resolves the excess ones during its
-// decode.
+// any order, so a lane whose request has more topics resolves the excess
+// ones during the decode.
 constexpr uint32_t kTopicQ = 4;
-constexpr int32_t kKPending = INT32_MIN;  // eval_kafka: parked topics, decided after the tile's lookups
-
-// What a request with parked topics needs once they are resolved.
-struct KPend {
-  uint32_t maxf;  // max of f(t) over the topics resolved during the decode
-  uint32_t cid;   // interned ClientID
-  int32_t kind;
-  int32_t version;
-  uint32_t nq;    // parked topics
-};
 
 // One record whose first `limit` bytes are readable at rec (LDS stage or HBM).
-// tq: this lane's topic column in LDS (kTopicQ u32 stage offsets of names,
-// stride 64), rec_so: rec's offset in the stage; used by the LDS-staged path
-// only, which returns kKPending with `pend` filled when topics were parked.
+// tq: this lane's topic column in LDS (kTopicQ u16 name offsets, stride 64);
+// used by the LDS-staged path only (stage offsets fit 16 bits).
 // spans: the header's per-kind candidate lists staged in LDS (kSpanLds);
 // kLds: rec is in the LDS stage.
 template <bool kLds>
 __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans, const uint8_t* rec,
-                                              uint64_t limit, const uint32_t* crc_tab, uint32_t* tq, uint32_t rec_so,
-                                              uint64_t gmask, bool& comp, KPend& pend, uint64_t (&prof)[5]) {
+                                              uint64_t limit, const uint32_t* crc_tab, uint16_t* tq,
+                                              uint64_t gmask, bool& comp, uint64_t (&prof)[5]) {
   if constexpr (kProf && kLds) prof[0] = __builtin_amdgcn_s_memtime();
   if (limit < 4) return L7M_VERDICT_PARSE_ERROR;
   const int32_t msize = static_cast<int32_t>((static_cast<uint32_t>(rec[0]) << 24) |
@@ -448,7 +432,7 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
       if (!tlen) {
         maxf = kNone;
       } else if (kLds && nq < kTopicQ) {
-        tq[64 * nq] = rec_so + toff;
+        tq[64 * nq] = static_cast<uint16_t>(toff);
         ++nq;
       } else {
         const uint32_t f = topic_first<kLds>(v, rec + toff, tlen, kok, kind, version, cid, gmask);
@@ -541,17 +525,54 @@ __device__ __forceinline__ int32_t eval_kafka(const KView& v, const Span* spans,
     } else if (ntop == 0) {
       first = first_in(v, spans[kKafkaKinds + kidx], 0, kNone, kind, false, version, true, cid, gmask);
     } else {
-      if constexpr (kProf && kLds) prof[1] += __builtin_amdgcn_s_memtime() - prof[0];
-      if (kLds && nq && maxf != kNone) {  // resolved after the tile's decode
-        pend.maxf = maxf;
-        pend.cid = cid;
-        pend.kind = kind;
-        pend.version = version;
-        pend.nq = nq;
-        return kKPending;
+      const uint64_t tr0 = kProf ? __builtin_amdgcn_s_memtime() : 0;
+      if constexpr (kProf && kLds) prof[1] += tr0 - prof[0];
+      // The parked topics' home-slot heads (hash, meta, first rule) are
+      // fetched together, so the lookups of a request cost one dependent
+      // L2 round trip instead of one per topic; the second pass compares
+      // names against the slots' inline prefixes (same cache line).
+      uint32_t hs[kTopicQ];
+      u32x4 hd[kTopicQ];
+#pragma unroll
+      for (uint32_t r = 0; r < kTopicQ; ++r) {
+        hs[r] = 0;
+        hd[r] = u32x4{0u, 0u, 0u, 0u};
+        if (r < nq && maxf != kNone) {
+          const uint32_t toff = tq[64 * r];
+          const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
+          if (tlen && tlen <= kMaxTopicLen && v.n_slots) {
+            hs[r] = load_name<kLds>(rec + toff, tlen).hash;
+            hd[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[0];
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < kTopicQ; ++r) {
+        if (r < nq && maxf != kNone) {
+          uint32_t f = kNone;
+          if (hs[r] && hd[r].x != 0) {
+            const uint32_t toff = tq[64 * r];
+            const uint32_t tlen = (static_cast<uint32_t>(rec[toff - 2]) << 8) | rec[toff - 1];
+            const uint32_t at = hs[r] & (v.n_slots - 1);
+            KafkaTopicSlot sl;
+            sl.hash = hd[r].x;
+            sl.meta = hd[r].y;
+            sl.r0 = hd[r].z;
+            sl.r0_client = hd[r].w;
+            const u32x4 pf = reinterpret_cast<const u32x4*>(v.slots + at)[1];
+            sl.pfx[0] = pf.x;
+            sl.pfx[1] = pf.y;
+            sl.pfx[2] = pf.z;
+            sl.pfx[3] = pf.w;
+            const Name nm = load_name<kLds, false>(rec + toff, tlen);
+            f = probe_topic(v, sl, hs[r], nm, rec + toff, tlen, kok, kind, version, cid, gmask);
+          }
+          maxf = f > maxf ? f : maxf;
+        }
       }
       const uint32_t j = first_in(v, spans[kidx], 0, maxf, kind, false, version, true, cid, gmask);
       first = j < maxf ? j : maxf;
+      if constexpr (kProf && kLds) prof[2] += __builtin_amdgcn_s_memtime() - tr0;
     }
   }
   return first == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(first);
@@ -621,13 +642,9 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   uint32_t* cli = ksmem + 256 + kSpanLds + kKindOkLds;
   const uint32_t cli_words = kCliLds ? h.n_clients * (sizeof(KafkaClientSlot) / 4) : 0u;
   uint32_t* ctr = cli + cli_words;
-  // per wave: 64 x kTopicQ parked-name columns (compacted in place into the
-  // tile's lookup list), 64 per-request maxima
-  uint32_t* tql = ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u) + wv * (64 * kTopicQ + 64);
-  uint32_t* mx = tql + 64 * kTopicQ;
-  uint32_t* tq = tql + lane;
-  uint8_t* stg = reinterpret_cast<uint8_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u) +
-                                            kKWaves * (64 * kTopicQ + 64)) + wv * (stage + 16u);
+  uint16_t* tq = reinterpret_cast<uint16_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
+  uint8_t* stg = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ) + wv * (stage + 16u);
+  tq += wv * 64 * kTopicQ + lane;
   if (kCliLds)
     for (uint32_t i = tid; i < cli_words; i += kKBlock) cli[i] = prog[h.off_clients + i];
   for (uint32_t i = tid; i < 2 * kKafkaKinds; i += kKBlock) ksmem[256 + kSpanLds + i] = prog[h.off_kind_ok + i];
@@ -736,11 +753,8 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
         }
       }
     }
-    bool comp = false;
-    KPend pend;
-    pend.nq = 0;
     if (lane < t.take) {
-      bool done = false;
+      bool done = false, comp = false;
       if (lane < t.k && onext - o >= 4) {
         const uint8_t* rec = stg + (o - t.base);
         const uint32_t msize = (static_cast<uint32_t>(rec[0]) << 24) | (static_cast<uint32_t>(rec[1]) << 16) |
@@ -749,101 +763,15 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
           verdict = static_cast<int32_t>(msize & 1u) - 1;
           done = true;
         } else if (msize < 0x7ffffff0u && ((4ull + msize + 3) & ~3ull) <= onext - o) {
-          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, static_cast<uint32_t>(o - t.base), gmask,
-                                     comp, pend, prof);
+          verdict = eval_kafka<true>(v, spans, rec, onext - o, crc_tab, tq, gmask, comp, prof);
           done = true;
         }
       }
       if (!done) {  // outside the staged window: decode from HBM
         const bool inb = (o & 3) == 0 && o + 4 <= arena_bytes;
-        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, 0, gmask, comp, pend,
-                                          prof)
+        verdict = inb ? eval_kafka<false>(v, spans, arena + o, arena_bytes - o, crc_tab, tq, gmask, comp, prof)
                       : L7M_VERDICT_PARSE_ERROR;
       }
-    }
-    if (verdict != kKPending) pend.nq = 0;
-    // the tile's parked topics, spread over the lanes
-    {
-      const uint64_t below = (1ull << lane) - 1ull;
-      const uint64_t b0 = __ballot(pend.nq & 1u), b1 = __ballot(pend.nq & 2u), b2 = __ballot(pend.nq & 4u);
-      const uint32_t total = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
-      if (total) {
-        const uint32_t pre = __popcll(b0 & below) + 2u * __popcll(b1 & below) + 4u * __popcll(b2 & below);
-        uint32_t e[kTopicQ];
-#pragma unroll
-        for (uint32_t r = 0; r < kTopicQ; ++r) e[r] = r < pend.nq ? tq[64 * r] : 0u;
-        wave_sync();
-#pragma unroll
-        for (uint32_t r = 0; r < kTopicQ; ++r)
-          if (r < pend.nq) tql[pre + r] = lane << 16 | e[r];
-        if (pend.nq) mx[lane] = pend.maxf;
-        wave_sync();
-        // the owners' request context, by shuffles (every lane takes part)
-        const uint32_t kvw = static_cast<uint32_t>(pend.kind & 0xffff) | static_cast<uint32_t>(pend.version) << 16;
-        uint32_t ent[kTopicQ], hs[kTopicQ];
-        u32x4 hd[kTopicQ];
-#pragma unroll
-        for (uint32_t r = 0; r < kTopicQ; ++r) {  // round 1: hash every entry, request its home slot's head
-          hs[r] = 0;
-          hd[r] = u32x4{0u, 0u, 0u, 0u};
-          ent[r] = kNone;
-          if (r * 64u < total) {
-            const uint32_t idx = r * 64u + lane;
-            if (idx < total) {
-              ent[r] = tql[idx];
-              const uint8_t* tn = stg + (ent[r] & 0xffffu);
-              const uint32_t tlen = (static_cast<uint32_t>(tn[-2]) << 8) | tn[-1];
-              if (tlen && tlen <= kMaxTopicLen && v.n_slots) {
-                hs[r] = load_name<true>(tn, tlen).hash;
-                hd[r] = reinterpret_cast<const u32x4*>(v.slots + (hs[r] & (v.n_slots - 1)))[0];
-              }
-            }
-          }
-        }
-#pragma unroll
-        for (uint32_t r = 0; r < kTopicQ; ++r) {  // round 2: compare, first applicable rule, fold
-          if (r * 64u < total) {
-            const uint32_t owner = ent[r] == kNone ? lane : ent[r] >> 16;
-            const uint32_t okv = __shfl(kvw, owner), ocid = __shfl(pend.cid, owner);
-            const uint64_t ogm = kGroups ? shfl64(gmask, owner) : ~0ull;
-            if (ent[r] != kNone) {
-              uint32_t f = kNone;
-              if (hs[r] && hd[r].x != 0) {
-                const uint8_t* tn = stg + (ent[r] & 0xffffu);
-                const uint32_t tlen = (static_cast<uint32_t>(tn[-2]) << 8) | tn[-1];
-                const uint32_t at = hs[r] & (v.n_slots - 1);
-                KafkaTopicSlot sl;
-                sl.hash = hd[r].x;
-                sl.meta = hd[r].y;
-                sl.r0 = hd[r].z;
-                sl.r0_client = hd[r].w;
-                const u32x4 pf = reinterpret_cast<const u32x4*>(v.slots + at)[1];
-                sl.pfx[0] = pf.x;
-                sl.pfx[1] = pf.y;
-                sl.pfx[2] = pf.z;
-                sl.pfx[3] = pf.w;
-                const int32_t okind = static_cast<int16_t>(okv & 0xffffu);
-                const int16_t over = static_cast<int16_t>(okv >> 16);
-                const uint64_t kok = v.kind_ok[(okind >= 0 && okind < 64) ? okind : 64];
-                const Name nm = load_name<true, false>(tn, tlen);
-                f = probe_topic(v, sl, hs[r], nm, tn, tlen, kok, okind, over, ocid, ogm);
-              }
-              atomicMax(mx + owner, f);
-            }
-          }
-        }
-        wave_sync();
-        if (pend.nq) {
-          const uint32_t maxf = mx[lane];
-          const uint32_t kidx = (pend.kind >= 0 && pend.kind < 64) ? static_cast<uint32_t>(pend.kind) : 64u;
-          const uint32_t j = first_in(v, spans[kidx], 0, maxf, pend.kind, false, static_cast<int16_t>(pend.version),
-                                      true, pend.cid, gmask);
-          const uint32_t first = j < maxf ? j : maxf;
-          verdict = first == kNone ? L7M_VERDICT_DENY : static_cast<int32_t>(first);
-        }
-      }
-    }
-    if (lane < t.take) {
       if (comp && verdict != L7M_VERDICT_PARSE_ERROR) {  // queue the request for the second pass
         const uint32_t at = atomicAdd(qhdr, 1u);
         if (at < qcap) crecs[at] = static_cast<uint32_t>(t.cur + lane);
@@ -906,7 +834,7 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const bool cli_lds = cli_words && cli_words * 4 <= kMaxCliLdsBytes;
   const size_t fixed = 4u * (256u + kSpanLds + kKindOkLds + (cli_lds ? cli_words : 0u) +
                              (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
-                       4u * kKWaves * (64 * kTopicQ + 64);
+                       2u * kKWaves * 64 * kTopicQ;
   size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
   stage &= ~size_t(15);
   if (stage > kKMaxStage) stage = kKMaxStage;

@@ -66,7 +66,7 @@ EXPORTED_SYMBOLS = (
     "l7m_proxy_stats_add", "l7m_compile_kafka_map", "l7m_eval_ids", "l7m_eval_device_ids",
     "l7m_batcher_eval_from", "l7m_proxy_stats_table_create", "l7m_proxy_stats_table_destroy",
     "l7m_proxy_stats_update", "l7m_proxy_stats_get", "l7m_http_access_log", "l7m_kafka_access_log",
-    "l7m_kafka_api_key_name",
+    "l7m_kafka_api_key_name", "l7m_batcher_get_profile",
 )
 
 
@@ -140,6 +140,11 @@ class _PortPolicy(ctypes.Structure):
 class _NetworkPolicy(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("ingress", ctypes.POINTER(_PortPolicy)), ("n_ingress", ctypes.c_size_t),
                 ("egress", ctypes.POINTER(_PortPolicy)), ("n_egress", ctypes.c_size_t)]
+
+
+class _BatcherProfile(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("fill_us", ctypes.c_double),
+                ("launch_us", ctypes.c_double), ("gpu_us", ctypes.c_double), ("wake_us", ctypes.c_double)]
 
 
 class _BatcherOpts(ctypes.Structure):
@@ -221,6 +226,7 @@ def _load() -> ctypes.CDLL:
     lib.l7m_batcher_eval_from.argtypes = [P, ctypes.c_char_p, sz, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]
     lib.l7m_batcher_eval_http.argtypes = [P, ctypes.POINTER(_HttpReq), ctypes.POINTER(ctypes.c_int32)]
     lib.l7m_batcher_stats.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.l7m_batcher_get_profile.argtypes = [P, ctypes.POINTER(_BatcherProfile)]
     lib.l7m_batcher_destroy.argtypes = [P]
     lib.l7m_batcher_destroy.restype = None
     lib.l7m_http_deny_body.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
@@ -676,6 +682,13 @@ class Batcher:
         b, r = ctypes.c_uint64(), ctypes.c_uint64()
         _lib.l7m_batcher_stats(self._h, ctypes.byref(b), ctypes.byref(r))
         return b.value, r.value
+
+    def profile(self) -> dict:
+        """Mean per-batch phases (l7m_batcher_get_profile), microseconds."""
+        p = _BatcherProfile()
+        _lib.l7m_batcher_get_profile(self._h, ctypes.byref(p))
+        return {"batches": p.batches, "requests": p.requests, "fill_us": p.fill_us, "launch_us": p.launch_us,
+                "gpu_us": p.gpu_us, "wake_us": p.wake_us}
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -346,10 +346,13 @@ int l7m_eval_device_ids(const l7m_ruleset* rs, const void* d_arena, size_t arena
  * (envoy/cilium_l7policy.cc:126-186) decide one request per call on the
  * connection's goroutine / worker thread.  l7m_batcher keeps that blocking
  * per-request call: any number of threads call l7m_batcher_eval; their
- * records share one l7m_eval, flushed when max_batch requests are pending or
- * the first has waited max_delay_us, while the next batch fills.  Up to
- * in_flight batches are evaluated at once (batch k+1's H2D copy overlaps
- * batch k's kernel); batches live in pinned host memory.  Destroying a
+ * records share one evaluation, flushed when max_batch requests are pending
+ * (or the batch's arena is full) or the first has waited max_delay_us, while
+ * the next batch fills.  Callers reserve their slot with one atomic
+ * compare-and-swap (no lock); batches live in pinned, device-mapped host
+ * memory that the kernels read and write in place (no copies); up to
+ * in_flight batches are evaluated at once, each flusher on its own stream,
+ * polling for completion; callers spin briefly, then sleep.  Destroying a
  * batcher with calls in flight is safe: pending batches are still decided,
  * later calls get L7M_EINVAL, and the memory is freed after the last caller
  * has returned.
@@ -376,6 +379,17 @@ int l7m_batcher_eval_from(l7m_batcher* b, const uint8_t* record, size_t len, uin
                           int32_t* verdict);
 int l7m_batcher_eval_http(l7m_batcher* b, const l7m_http_request* req, int32_t* verdict);
 int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests);
+/* Where a batch's time goes (means since creation): fill = first request
+ * appended -> batch closed by a flusher; launch = closed -> kernels enqueued
+ * (l7m_eval_device on the batch's pinned, device-mapped buffers: records read
+ * and verdicts written in place); gpu = enqueued -> completion observed by the
+ * flusher (event polling); wake = completion -> the caller has its verdict
+ * (mean per request). */
+typedef struct {
+  uint64_t batches, requests;
+  double fill_us, launch_us, gpu_us, wake_us;
+} l7m_batcher_profile;
+int l7m_batcher_get_profile(l7m_batcher* b, l7m_batcher_profile* out);
 void l7m_batcher_destroy(l7m_batcher* b);
 
 /* ---- verdict side effects (host; for requests the GPU decided) ------------
