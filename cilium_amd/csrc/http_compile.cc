@@ -644,6 +644,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     img += (words + 3) & ~uint64_t(3);  // 16-byte granules
     return static_cast<uint32_t>(o);
   };
+  img_take(256);  // image words [0, 256): the zero dead row of every LDS slot table (program.h kLdsRowShift)
   const uint32_t lds_dfas = img_take(static_cast<uint64_t>(ndt) * sizeof(DfaDesc) / 4);
   const uint32_t lds_fields = img_take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
   const uint32_t lds_name_field = img_take(name_field.size());
@@ -710,6 +711,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     const uint64_t need = ((d.n_slots + 3) & ~3ull) + ((half_es + 3) & ~3ull) + ((half_latch + 3) & ~3ull);
     const bool es16 = d.sets.size() < kEs16Latched && all[k].npats < kEs16Latched;
     const bool es8 = d.sets.size() < kEs8Latched && all[k].npats < kEs16Latched;
+    if (img + d.n_slots > kLdsTableWords) continue;  // rows are 16-bit byte addresses (program.h)
     const uint64_t need8 = ((d.n_slots + 3) & ~3ull) + ((half_latch + 3) & ~3ull);
     if (es8 && img + need8 <= budget) {  // end codes ride in the slot entries
       dd[k].lds_table = img_take(d.n_slots);
@@ -910,8 +912,8 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
         }
     }
     if (dd[k].lds_table != kNone) {
-      // the LDS copy names rows by image word index (program.h kLdsRowShift),
-      // with the target state's end code when it fits 8 bits
+      // the LDS copy names rows by image byte address (program.h
+      // kLdsRowShift), with the target state's end code when it fits 8 bits
       const uint32_t t0 = dd[k].lds_table;
       const bool in_entry = dd[k].lds_es == kLdsEsInEntry;
       auto es8 = [&](uint32_t base) -> uint32_t {
@@ -919,8 +921,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       };
       for (uint32_t s = 0; s < d.n_slots; ++s) {
         const uint32_t e = d.table[s], next = e >> 8;
-        I[t0 + s] = next ? ((t0 + next) << kLdsRowShift) | (in_entry ? es8(next) << 8 : 0u) | (e & 0xffu)
-                         : (t0 << kLdsRowShift);
+        I[t0 + s] = next ? ((4 * (t0 + next)) << kLdsRowShift) | (in_entry ? es8(next) << 8 : 0u) | (e & 0xffu) : 0u;
       }
       if (in_entry && d.start_base) dd[k].start_es8 = es8(d.start_base);
       for (uint32_t s = 0; dd[k].lds_es != kNone && !in_entry && s < d.n_slots; ++s)

@@ -154,7 +154,7 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
       if (slot->done) (void)hipEventDestroy(slot->done);
       slot->qhdr = nullptr;
       slot->done = nullptr;
-      if (hipMalloc(reinterpret_cast<void**>(&slot->qhdr), 16) != hipSuccess ||
+      if (hipMalloc(reinterpret_cast<void**>(&slot->qhdr), 16) != hipSuccess || hipMemset(slot->qhdr, 0, 16) != hipSuccess ||
           hipEventCreateWithFlags(&slot->done, hipEventDisableTiming) != hipSuccess) {
         if (slot->qhdr) (void)hipFree(slot->qhdr);
         slot->qhdr = nullptr;
@@ -167,8 +167,9 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
     if (g.workers && !slot->recs &&
         hipMalloc(reinterpret_cast<void**>(&slot->recs), kCodecQueueCap * sizeof(uint32_t)) == hipSuccess)
       slot->cap = kCodecQueueCap;  // retried on later launches when it failed
+    // the queue header is zero here: reset by the previous user's second
+    // pass (kafka_codec_kernel) or by the memset after a launch without one
     hipError_t e = hipStreamWaitEvent(stream, slot->done, 0);
-    if (e == hipSuccess) e = hipMemsetAsync(slot->qhdr, 0, 16, stream);
     if (e != hipSuccess) {
       slot->busy = false;
       return e;
@@ -182,10 +183,13 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
   }
   hipError_t e = launch_kafka(dprog, h, arena, arena_bytes, offs, n, verdicts, hits, stream, cus, flags, cq, ids);
   std::lock_guard<std::mutex> lk(g.mu);
-  if (e == hipSuccess && n && !(flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) && cq.cap) {
+  if (e == hipSuccess && n && !(flags & (L7M_FLAG_DIAG_COPY_ONLY | L7M_FLAG_DIAG_WALK_ONLY)) && cq.cap &&
+      cq.workers) {
     e = hipStreamWaitEvent(stream, g.p2_done, 0);
     if (e == hipSuccess) e = launch_kafka_codec(dprog, arena, arena_bytes, offs, n, verdicts, hits, stream, cq);
     if (e == hipSuccess) e = hipEventRecord(g.p2_done, stream);
+  } else if (e == hipSuccess && n) {
+    e = hipMemsetAsync(slot->qhdr, 0, 16, stream);  // no second pass to reset the queue header
   }
   const hipError_t e2 = hipEventRecord(slot->done, stream);
   if (e == hipSuccess) e = e2;

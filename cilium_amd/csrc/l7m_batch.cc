@@ -245,8 +245,9 @@ struct l7m_batcher {
       l7m_ruleset_get_info(r, &info);
       int rc = dev_ok ? L7M_OK : L7M_EDEVICE;
       if (rc == L7M_OK)
-        rc = l7m_eval_device_ids(r, b->d_arena, bytes, b->d_offs, cnt,
-                                 info.proto == L7M_PROTO_KAFKA ? b->d_ids : nullptr, b->d_verd, nullptr, stream, 0);
+        rc = info.proto == L7M_PROTO_KAFKA
+                 ? l7m_eval_device_ids(r, b->d_arena, bytes, b->d_offs, cnt, b->d_ids, b->d_verd, nullptr, stream, 0)
+                 : l7m_eval_device(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, nullptr, stream, 0);
       const int64_t t_launch = now_ns();
       if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
       if (rc == L7M_OK) {

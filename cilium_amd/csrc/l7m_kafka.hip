@@ -911,6 +911,14 @@ __global__ __launch_bounds__(64) void kafka_codec_kernel(const uint32_t* __restr
       atomicAdd(hits + 1, 1ull);  // -2 and -3 share slot 1
     }
   }
+  // The last worker to finish resets the queue header for the next launch on
+  // this queue (which waits for this kernel): no memset per launch.
+  __threadfence();
+  if (atomicAdd(qhdr + 2, 1u) == gridDim.x - 1) {
+    __hip_atomic_store(qhdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(qhdr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(qhdr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace

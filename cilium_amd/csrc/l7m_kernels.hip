@@ -68,12 +68,27 @@ struct LdsSrc {
   const uint32_t* w;  // word 0 of the record in the wave's LDS stage
   __device__ __forceinline__ uint32_t word(uint32_t i) const { return w[i]; }
   __device__ __forceinline__ uint32_t byte(uint32_t i) const { return reinterpret_cast<const uint8_t*>(w)[i]; }
+#ifdef L7M_ALIGNED_WORDS
+  // bytes [p, p + 4) from two 4-byte-aligned reads (a b64 read off its 8-byte
+  // alignment is replayed by the LDS)
+  __device__ __forceinline__ uint32_t word_u(uint32_t p) const {
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(w) + (p & ~3u));
+    return __builtin_amdgcn_alignbyte(a[1], a[0], p & 3u);
+  }
+#else
+  __device__ __forceinline__ uint32_t word_u(uint32_t p) const {
+    return byte(p) | byte(p + 1) << 8 | byte(p + 2) << 16 | byte(p + 3) << 24;
+  }
+#endif
 };
 struct GlbSrc {
   static constexpr bool kLds = false;
   const uint32_t* w;  // word 0 of the record in HBM
   __device__ __forceinline__ uint32_t word(uint32_t i) const { return __builtin_nontemporal_load(w + i); }
   __device__ __forceinline__ uint32_t byte(uint32_t i) const { return reinterpret_cast<const uint8_t*>(w)[i]; }
+  __device__ __forceinline__ uint32_t word_u(uint32_t p) const {
+    return byte(p) | byte(p + 1) << 8 | byte(p + 2) << 16 | byte(p + 3) << 24;
+  }
 };
 
 // End code of a finished walk (final base, slot of the last transition taken
@@ -201,43 +216,113 @@ __device__ __forceinline__ uint32_t walk_hbm(const uint32_t* __restrict__ img, c
 }
 
 // A walk through an LDS slot table, re-encoded by the compiler for it
-// (program.h kLdsRowShift): e = (image word index of the next row << 16) |
-// label, the dead row being the table's own row 0 (no label matches there).
-// A step is
-//     slot = (sel >> 16) + b;  e = img[slot];  sel = label(e) == b ? e : dead
-// with the word / byte selects folded into SDWA operands.  `slast` is the
-// slot of the last transition taken from a multi-pattern row (below lim).
+// (program.h kLdsRowShift): e = (image byte address of the next row << 16) |
+// es8 << 8 | label, 0 for a dead transition (row 0: the zero dead row at the
+// image start).  The label check of a step is folded into the address of the
+// next read: with bp the byte the last read consumed,
+//     a = row(e) + 4 b,  byte 3 of a = label(e) ^ bp;  e = lds[a]
+// three VALU ops (SDWA byte / half-word selects, the xor writing byte 3 in
+// place): a wrong label puts the address 16 MiB past the LDS, where a read
+// returns 0, the dead row (measured: tools/lds_chain_bench.hip).  The walk is
+// VALU-issue bound at 16 waves per CU (SQ_ACTIVE_INST_VALU ~60 % of the SIMD
+// cycles), so VALU ops per byte are the cost: 3 here, 6 in the compare /
+// select form.  `slast` (the slot of the last transition taken from a
+// multi-pattern row, below lim) costs two more, so it is tracked only in the
+// 8-byte blocks that start with a lane in the multi-pattern region: states
+// never return there once they leave it (dfa_pack.h latching).
+// The image must start at LDS address 0 (the kernels' only LDS array).
+typedef __attribute__((address_space(3))) const uint32_t* lds_cptr;
+__device__ __forceinline__ uint32_t lds_at(uint32_t byte_addr) {
+  return *reinterpret_cast<lds_cptr>(static_cast<uintptr_t>(byte_addr));
+}
+
+// One step on byte SEL of W, the previous byte being PSEL of P.
+#define L7M_OSTEP(W, SEL, P, PSEL, TRACK)                                                                      \
+  {                                                                                                            \
+    uint32_t t_;                                                                                               \
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" SEL        \
+        : "=v"(t_)                                                                                             \
+        : "v"(W));                                                                                             \
+    asm("v_add_u32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"         \
+        : "+v"(t_)                                                                                             \
+        : "v"(e));                                                                                             \
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:" PSEL \
+        : "+v"(t_)                                                                                             \
+        : "v"(e), "v"(P));                                                                                     \
+    if (TRACK) slast = (e >> kLdsRowShift) < lim ? t_ : slast;                                                 \
+    e = lds_at(t_);                                                                                            \
+  }
+
 struct LdsChain {
-  uint32_t sel, dead, lim, slast;
+  uint32_t e;      // the last entry read
+  uint32_t pw;     // byte 3: the byte that read consumed
+  uint32_t lim;    // byte address of the first latched row
+  uint32_t t0;     // the table's image word offset
+  uint32_t slast;  // slot byte address (kNone: none)
   __device__ __forceinline__ void init(const DfaDesc& dd) {
-    dead = dd.lds_table << kLdsRowShift;
-    lim = dd.lds_table + dd.region;
-    sel = ((dd.lds_table + dd.start_base) << kLdsRowShift) | (dd.start_es8 << 8);
+    t0 = dd.lds_table;
+    lim = 4 * (dd.lds_table + dd.region);
+    e = ((4 * (dd.lds_table + dd.start_base)) << kLdsRowShift) | (dd.start_es8 << 8);  // label 0
+    pw = 0;
     slast = kNone;
   }
-  __device__ __forceinline__ void step(const uint32_t* __restrict__ img, uint32_t b) {
-    uint32_t s = (sel >> kLdsRowShift) + b;
-    asm("" : "+v"(s));  // one SDWA add, then the scale
-    const uint32_t e = img[s];
-    slast = (sel >> kLdsRowShift) < lim ? s : slast;
-    sel = (e & 0xffu) == b ? e : dead;
+  __device__ __forceinline__ bool dead_now() const {
+    return (e >> kLdsRowShift) == 0 || (e & 0xffu) != (pw >> 24);
   }
-  __device__ __forceinline__ bool dead_now() const { return sel == dead; }
+  template <class Src>
+  __device__ __forceinline__ static uint32_t word_at(const Src& src, uint32_t p) {
+    return src.word_u(p);
+  }
   // continue the walk over bytes [k, len) of the field at pos
   template <class Src>
-  __device__ __forceinline__ void run(const uint32_t* __restrict__ img, const Src& src, uint32_t pos, uint32_t len,
-                                      uint32_t k) {
-#define L7M_STEP(B) step(img, (B));
-    L7M_WALK_BYTES(L7M_STEP, dead_now())
-#undef L7M_STEP
+  __device__ __forceinline__ void run(const Src& src, uint32_t pos, uint32_t len, uint32_t k) {
+    for (; k + 8 <= len; k += 8) {
+      const uint32_t w0 = word_at(src, pos + k), w1 = word_at(src, pos + k + 4);
+      if (__any((e >> kLdsRowShift) < lim)) {  // some lane may still leave the multi-pattern region
+        L7M_OSTEP(w0, "BYTE_0", pw, "BYTE_3", true)
+        L7M_OSTEP(w0, "BYTE_1", w0, "BYTE_0", true)
+        L7M_OSTEP(w0, "BYTE_2", w0, "BYTE_1", true)
+        L7M_OSTEP(w0, "BYTE_3", w0, "BYTE_2", true)
+        L7M_OSTEP(w1, "BYTE_0", w0, "BYTE_3", true)
+        L7M_OSTEP(w1, "BYTE_1", w1, "BYTE_0", true)
+        L7M_OSTEP(w1, "BYTE_2", w1, "BYTE_1", true)
+        L7M_OSTEP(w1, "BYTE_3", w1, "BYTE_2", true)
+      } else {
+        L7M_OSTEP(w0, "BYTE_0", pw, "BYTE_3", false)
+        L7M_OSTEP(w0, "BYTE_1", w0, "BYTE_0", false)
+        L7M_OSTEP(w0, "BYTE_2", w0, "BYTE_1", false)
+        L7M_OSTEP(w0, "BYTE_3", w0, "BYTE_2", false)
+        L7M_OSTEP(w1, "BYTE_0", w0, "BYTE_3", false)
+        L7M_OSTEP(w1, "BYTE_1", w1, "BYTE_0", false)
+        L7M_OSTEP(w1, "BYTE_2", w1, "BYTE_1", false)
+        L7M_OSTEP(w1, "BYTE_3", w1, "BYTE_2", false)
+      }
+      pw = w1;
+      if (dead_now()) return;
+    }
+    if (k + 4 <= len) {
+      const uint32_t w0 = word_at(src, pos + k);
+      L7M_OSTEP(w0, "BYTE_0", pw, "BYTE_3", true)
+      L7M_OSTEP(w0, "BYTE_1", w0, "BYTE_0", true)
+      L7M_OSTEP(w0, "BYTE_2", w0, "BYTE_1", true)
+      L7M_OSTEP(w0, "BYTE_3", w0, "BYTE_2", true)
+      pw = w0;
+      k += 4;
+    }
+    for (; k < len; ++k) {
+      const uint32_t b = src.byte(pos + k);
+      L7M_OSTEP(b, "BYTE_0", pw, "BYTE_3", true)
+      pw = b << 24;
+    }
   }
   __device__ __forceinline__ uint32_t code(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
                                            const DfaDesc& dd) const {
-    const uint32_t t0 = dead >> kLdsRowShift;
-    const uint32_t base = (sel >> kLdsRowShift) - t0, last = slast == kNone ? kNone : slast - t0;
+    const bool ok = !dead_now();
+    const uint32_t base = ok ? (e >> (kLdsRowShift + 2)) - t0 : 0u;
+    const uint32_t last = slast == kNone ? kNone : ((slast & 0xffffffu) >> 2) - t0;
     if (dd.lds_es == kLdsEsInEntry) {  // the end code came with the last entry read
       if (!base) return 0;
-      const uint32_t es = (sel >> 8) & 0xffu;
+      const uint32_t es = (e >> 8) & 0xffu;
       if (es != kEs8Latched) return es;
       const uint16_t* I16 = reinterpret_cast<const uint16_t*>(img);
       return kLatchedBit | (last == kNone ? dd.start_latch : I16[dd.lds_latch + last]);
@@ -245,13 +330,14 @@ struct LdsChain {
     return end_code<true>(img, prog, dd, base, last);
   }
 };
+#undef L7M_OSTEP
 
 template <class Src>
 __device__ __forceinline__ uint32_t walk_lds(const uint32_t* __restrict__ img, const uint32_t* __restrict__ prog,
                                              const DfaDesc& dd, const Src& src, uint32_t pos, uint32_t len) {
   LdsChain c;
   c.init(dd);
-  if (dd.start_base) c.run(img, src, pos, len, 0);
+  if (dd.start_base) c.run(src, pos, len, 0);
   return c.code(img, prog, dd);
 }
 
@@ -1239,7 +1325,8 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   const dim3 grid(static_cast<uint32_t>(blocks));
   const bool reg = h.n_dfas <= kRegDfas;
   if (flags & (L7M_FLAG_DIAG_WALK_ONLY | L7M_FLAG_DIAG_COPY_ONLY)) {  // diagnostic ablations
-    if (!reg) return hipErrorInvalidValue;
+    // (register end codes only; no search automata, no slow-path queue)
+    if (!reg || h.search || h.n_slow) return hipErrorInvalidValue;
     if (flags & L7M_FLAG_DIAG_COPY_ONLY)
       return launch_one<kNoHits, 8, 2>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
     return launch_one<kNoHits, 8, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);

@@ -112,11 +112,15 @@ struct CandEntry {
 static_assert(sizeof(CandEntry) == 64, "cand entry is 16 words");
 constexpr uint32_t kLatchedBit = 0x80000000u;
 constexpr uint32_t kEs16Latched = 0xffffu;
-// The LDS copy of a slot table names rows by image word index: entry =
-// (lds_table + next base) << kLdsRowShift | label, a dead transition (or
-// unowned slot) = lds_table << kLdsRowShift (the table's row 0, where no
-// label matches).  The image is < 64 Ki words (kLdsBytes), so indices fit.
+// The LDS copy of a slot table names rows by image BYTE address: entry =
+// 4 * (lds_table + next base) << kLdsRowShift | label, a dead transition (or
+// unowned slot) = 0, i.e. row 0 = image words [0, 256), which are zero (the
+// dead row shared by all tables; every read there is 0 again).  A walk step
+// adds 4 * byte to the entry's upper half and reads (l7m_kernels.hip
+// LdsChain).  Tables therefore end below image word kLdsTableWords (byte
+// addresses fit 16 bits).
 constexpr uint32_t kLdsRowShift = 16;
+constexpr uint32_t kLdsTableWords = 16384;
 // When a DFA has fewer than 255 end codes its LDS entries also carry the end
 // code of the state they lead to: entry = row << 16 | es8 << 8 | label, es8 =
 // es (0 = no match) or kEs8Latched; its lds_es is then kLdsEsInEntry and the

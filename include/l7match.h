@@ -307,7 +307,9 @@ size_t l7m_pack_http(const l7m_http_request* reqs, size_t n, uint8_t* arena, siz
 
 /* ---- evaluation flags ------------------------------------------------------
  * 0 for normal use.  The DIAG flags select profiling ablations of the HTTP
- * kernel whose verdicts are NOT valid (used by bench.py --diag). */
+ * kernel whose verdicts are NOT valid (used by bench.py --diag).  HTTP
+ * programs with more than 8 value automata, RE2-dialect search automata or
+ * slow-path rules have no ablation build: the call returns L7M_EDEVICE. */
 #define L7M_FLAG_DIAG_WALK_ONLY 0x40000000u  /* stop after the DFA walks       */
 #define L7M_FLAG_DIAG_COPY_ONLY 0x80000000u  /* stop after staging/validation  */
 

@@ -111,8 +111,8 @@ class HttpProgram:
         last = KNONE
         es8 = d["start_es8"]
         if lds:
-            # LDS copy (program.h kLdsRowShift): e = (image row index << 16) |
-            # es8 << 8 | label, the table's row 0 is the dead row
+            # LDS copy (program.h kLdsRowShift): e = (image row byte address
+            # << 16) | es8 << 8 | label, 0 for dead transitions
             t0 = d["lds_table"]
             n = len(data)
             st = [base, es8, last]
@@ -123,7 +123,8 @@ class HttpProgram:
                 e = self.img[t0 + slot]
                 if bs < d["region"]:
                     st[2] = slot
-                st[0], st[1] = ((e >> 16) - t0, (e >> 8) & 0xFF) if (e & 0xFF) == c else (0, 0)
+                ok = (e & 0xFF) == c and (e >> 16) != 0  # row 0: the shared dead row
+                st[0], st[1] = ((e >> 16) // 4 - t0, (e >> 8) & 0xFF) if ok else (0, 0)
 
             k = 0
             while k < n and st[0]:

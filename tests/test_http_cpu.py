@@ -246,7 +246,7 @@ def test_compiler_table_only_lds_placement_matches_oracle():
     latches is placed alone (end codes stay in the program)."""
     rules = W.rules(2, n_rules=400)
     arena, offs = W.requests(2, 0, 1500, n_rules=400)
-    rs = L.RuleSet.compile_http(rules, lds_budget_bytes=12288)
+    rs = L.RuleSet.compile_http(rules, lds_budget_bytes=13312)
     P = HttpProgram(rs.program())
     assert any(d["lds_table"] != 0xFFFFFFFF and d["lds_es"] == 0xFFFFFFFF for d in P.dfas)
     assert (P.eval(arena, offs) == HttpOracle(rules).eval(arena, offs)).all()

@@ -53,7 +53,7 @@ template <int kForm>
 __global__ __launch_bounds__(kBlock) void chain_kernel(const uint32_t* __restrict__ tab, uint32_t steps,
                                                        uint32_t* __restrict__ out, unsigned long long* __restrict__ cyc) {
   extern __shared__ __align__(16) uint32_t smem[];
-  for (uint32_t i = threadIdx.x; i < kImgWords; i += kBlock) smem[i] = tab[kForm * kImgWords + i];
+  for (uint32_t i = threadIdx.x; i < kImgWords; i += kBlock) smem[i] = tab[(kForm ? 1 : 0) * kImgWords + i];
   __syncthreads();
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
   uint32_t seed = mix(tid * 2654435761u + 17u);
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(const uint32_t* __restric
       }
       acc += sel;
     }
-  } else {
+  } else if (kForm == 1) {
     const uint32_t dead = 0;     // byte address of the dead row
     uint32_t e = (256u * 4u) << 16;  // row 1 (byte address), label 0
     uint32_t bprev = 0;
@@ -96,9 +96,52 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(const uint32_t* __restric
       acc += e;
     }
   }
+  if (kForm == 2) {
+    // OOR form: a = row(e) + 4 b with byte 3 = label(e) ^ b_prev (SDWA,
+    // other bytes preserved), so a label mismatch addresses past the LDS
+    // and reads 0 (the dead row at address 0)
+    uint32_t e = (256u * 4u) << 16;  // row 1 (byte address), label 0
+    uint32_t wprev = 0;               // packed bytes of the previous block (byte 3 = b_prev of step 0)
+    for (uint32_t k = 0; k < steps; k += 8) {
+      const uint32_t w0 = mix(seed + k), w1 = mix(seed + k + 4);
+#define STEP(W, SEL, P, PSEL)                                                                           \
+  {                                                                                                    \
+    uint32_t t;                                                                                        \
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" SEL \
+        : "=v"(t) : "v"(W));                                                                            \
+    asm("v_add_u32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"  \
+        : "+v"(t) : "v"(e));                                                                            \
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0 src1_sel:" \
+        PSEL : "+v"(t) : "v"(e), "v"(P));                                                               \
+    e = lds_at(t);                                                                                     \
+  }
+      STEP(w0, "BYTE_0", wprev, "BYTE_3")
+      STEP(w0, "BYTE_1", w0, "BYTE_0")
+      STEP(w0, "BYTE_2", w0, "BYTE_1")
+      STEP(w0, "BYTE_3", w0, "BYTE_2")
+      STEP(w1, "BYTE_0", w0, "BYTE_3")
+      STEP(w1, "BYTE_1", w1, "BYTE_0")
+      STEP(w1, "BYTE_2", w1, "BYTE_1")
+      STEP(w1, "BYTE_3", w1, "BYTE_2")
+#undef STEP
+      wprev = w1;
+      acc += e;
+    }
+  }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   out[tid] = acc;
   if ((threadIdx.x & 63) == 0) atomicAdd(cyc, static_cast<unsigned long long>(t1 - t0));
+}
+
+// Reads LDS words past the allocation (addresses 160 KiB, 2^18, 2^24 + 4):
+// the OOR form relies on such reads returning 0.
+__global__ void oor_kernel(uint32_t* out) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  for (uint32_t i = threadIdx.x; i < kLdsBytes / 4; i += blockDim.x) smem[i] = 0xdeadbeefu;
+  __syncthreads();
+  uint32_t a = threadIdx.x == 0 ? kLdsBytes : threadIdx.x == 1 ? (1u << 18) : threadIdx.x == 2 ? (1u << 24) + 4u : 0u;
+  asm volatile("" : "+v"(a));
+  out[threadIdx.x] = lds_at(a);
 }
 
 int main() {
@@ -127,7 +170,17 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int form = 0; form < 2; ++form) {
+  {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(oor_kernel), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
+    hipLaunchKernelGGL(oor_kernel, dim3(1), dim3(64), kLdsBytes, 0, dout);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    uint32_t r[4];
+    CK(hipMemcpy(r, dout, 16, hipMemcpyDeviceToHost));
+    std::printf("oor reads: @160K %08x @2^18 %08x @2^24+4 %08x in-range %08x\n", r[0], r[1], r[2], r[3]);
+  }
+  CK(hipFuncSetAttribute(reinterpret_cast<const void*>(chain_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
+  for (int form = 0; form < 3; ++form) {
     float best = 1e30f;
     unsigned long long cy = 0;
     for (int rep = 0; rep < 5; ++rep) {
@@ -135,8 +188,10 @@ int main() {
       CK(hipEventRecord(e0, 0));
       if (form == 0)
         hipLaunchKernelGGL(chain_kernel<0>, dim3(grid), dim3(kBlock), kLdsBytes, 0, dtab, steps, dout, dcyc);
-      else
+      else if (form == 1)
         hipLaunchKernelGGL(chain_kernel<1>, dim3(grid), dim3(kBlock), kLdsBytes, 0, dtab, steps, dout, dcyc);
+      else
+        hipLaunchKernelGGL(chain_kernel<2>, dim3(grid), dim3(kBlock), kLdsBytes, 0, dtab, steps, dout, dcyc);
       CK(hipGetLastError());
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
@@ -147,7 +202,7 @@ int main() {
     }
     const double waves = static_cast<double>(grid) * (kBlock / 64);
     std::printf("form %s: %.3f ms, %.1f wave-cycles per step (s_memtime), %.2f ns per step per wave\n",
-                form ? "select" : "check", best, static_cast<double>(cy) / waves / steps,
+                form == 2 ? "oor" : form ? "select" : "check", best, static_cast<double>(cy) / waves / steps,
                 best * 1e6 / steps);
   }
   std::printf("cus %d clock_khz %d\n", cus, clk);
