@@ -30,7 +30,9 @@
 // pkg/proxy/redirect.go:68-74): batches flushed afterwards use the new rules.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <cstddef>
@@ -40,6 +42,11 @@
 #include <vector>
 
 #include "../../include/l7match.h"
+#include "l7m_device.h"
+
+namespace l7m {
+bool resident_program(l7m_ruleset* rs, const uint32_t** dprog, int* kind, uint32_t* stage, uint64_t* serial);
+}
 
 namespace {
 
@@ -152,6 +159,127 @@ struct l7m_batcher {
   // statistics (l7m_batcher_stats / l7m_batcher_get_profile)
   std::atomic<uint64_t> batches{0}, requests{0}, fill_ns{0}, launch_ns{0}, gpu_ns{0}, wake_ns{0};
 
+  // Resident evaluator (l7m_kernels.hip http_resident_kernel): batches of
+  // up to kResidentMax HTTP records whose program it can serve are posted to
+  // a workgroup that stays on the GPU, instead of launching a kernel each.
+  static constexpr uint32_t kResidentMax = 1024;
+  struct Resident {
+    std::mutex mu;
+    l7m::ResidentBox* box = nullptr;   // pinned host memory
+    l7m::ResidentBox* dbox = nullptr;  // its device address
+    hipStream_t stream = nullptr;
+    uint32_t* qhdr = nullptr;          // device: the Kafka instantiations' queue counter
+    hipEvent_t end = nullptr;          // recorded after the running instance
+    bool running = false;
+    uint64_t posted = 0;
+    std::vector<l7m_ruleset*> held;    // programs the running instance may have read (kept alive until it ends)
+    l7m_ruleset* slot_rs[l7m::kResidentSlots] = {};  // rule set of each posted slot
+    bool ok = false;
+  } res;
+  // (res.mu held)
+  void resident_hold_locked(l7m_ruleset* r) {
+    if (std::find(res.held.begin(), res.held.end(), r) == res.held.end()) {
+      l7m_retain(r);
+      res.held.push_back(r);
+    }
+  }
+
+  void resident_init() {
+    (void)hipSetDevice(device);
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(l7m::ResidentBox), hipHostMallocMapped) != hipSuccess || !p) return;
+    std::memset(p, 0, sizeof(l7m::ResidentBox));
+    res.box = static_cast<l7m::ResidentBox*>(p);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d ||
+        hipStreamCreateWithFlags(&res.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&res.end, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&res.qhdr), 16) != hipSuccess || hipMemset(res.qhdr, 0, 16) != hipSuccess)
+      return;
+    res.dbox = static_cast<l7m::ResidentBox*>(d);
+    res.ok = !std::getenv("L7M_NO_RESIDENT");
+  }
+  void resident_fini() {
+    if (res.box) {
+      __atomic_store_n(&res.box->quit, 1ull, __ATOMIC_RELEASE);
+      if (res.running && res.end) (void)hipEventSynchronize(res.end);
+    }
+    for (l7m_ruleset* r : res.held) l7m_release(r);
+    res.held.clear();
+    if (res.end) (void)hipEventDestroy(res.end);
+    if (res.qhdr) (void)hipFree(res.qhdr);
+    if (res.stream) (void)hipStreamDestroy(res.stream);
+    if (res.box) (void)hipHostFree(res.box);
+  }
+  // (res.mu held) the running instance has ended: its cached programs may go
+  void resident_reap_locked() {
+    if (res.running && hipEventQuery(res.end) == hipSuccess) {
+      res.running = false;
+      for (l7m_ruleset* r : res.held) l7m_release(r);
+      res.held.clear();
+    }
+  }
+  // (res.mu held) a workgroup for the oldest pending slot
+  bool resident_launch_locked() {
+    const uint64_t first = __atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) + 1;
+    if (first > res.posted) return true;
+    const int kind = static_cast<int>(
+        __atomic_load_n(&res.box->slots[first % l7m::kResidentSlots].kind, __ATOMIC_ACQUIRE));
+    if (l7m::launch_resident(res.dbox, first, kind, res.qhdr, res.stream) != hipSuccess ||
+        hipEventRecord(res.end, res.stream) != hipSuccess)
+      return false;
+    res.running = true;
+    for (uint64_t q = first; q <= res.posted; ++q) resident_hold_locked(res.slot_rs[q % l7m::kResidentSlots]);
+    return true;
+  }
+  // Evaluate batch b (cnt records, bytes) on the resident workgroup.
+  int resident_eval(l7m_ruleset* r, const uint32_t* dprog, int kind, uint32_t stage, uint64_t serial, Batch* b,
+                    uint32_t cnt, uint64_t bytes) {
+    uint64_t seq;
+    {
+      std::unique_lock<std::mutex> lk(res.mu);
+      while (res.posted - __atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= l7m::kResidentSlots) {
+        lk.unlock();  // ring full (more flushers than slots): let the workgroup catch up
+        cpu_relax();
+        lk.lock();
+      }
+      seq = ++res.posted;
+      l7m::ResidentSlot& sl = res.box->slots[seq % l7m::kResidentSlots];
+      auto put = [](uint64_t* f, uint64_t v) { __atomic_store_n(f, v, __ATOMIC_RELAXED); };
+      put(&sl.kind, static_cast<uint64_t>(kind));
+      put(&sl.gen, serial);
+      put(&sl.prog, reinterpret_cast<uint64_t>(dprog));
+      put(&sl.arena, reinterpret_cast<uint64_t>(b->d_arena));
+      put(&sl.arena_bytes, bytes);
+      put(&sl.offs, reinterpret_cast<uint64_t>(b->d_offs));
+      put(&sl.n, cnt);
+      put(&sl.verdicts, reinterpret_cast<uint64_t>(b->d_verd));
+      put(&sl.stage, stage);
+      put(&sl.ids, reinterpret_cast<uint64_t>(b->d_ids));
+      put(&sl.result, 0);
+      res.slot_rs[seq % l7m::kResidentSlots] = r;
+      resident_hold_locked(r);
+      __atomic_store_n(&res.box->post_seq, seq, __ATOMIC_RELEASE);
+      resident_reap_locked();
+      if (!res.running && !resident_launch_locked()) return L7M_EDEVICE;
+    }
+    // L7M_OK, or 1: the workgroup asks for the normal launches (Kafka
+    // batches with compressed message sets need the codec pass)
+    auto outcome = [&]() -> int {
+      return __atomic_load_n(&res.box->slots[seq % l7m::kResidentSlots].result, __ATOMIC_ACQUIRE) ? 1 : L7M_OK;
+    };
+    for (uint32_t spin = 0;; ++spin) {
+      if (__atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= seq) return outcome();
+      if ((spin & 63) == 63) {  // the instance may have exited (idle, or another instantiation)
+        std::lock_guard<std::mutex> g(res.mu);
+        if (__atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= seq) return outcome();
+        resident_reap_locked();
+        if (!res.running && !resident_launch_locked()) return L7M_EDEVICE;
+      }
+      cpu_relax();
+    }
+  }
+
   Batch* fresh() {
     {
       std::lock_guard<std::mutex> g(pool_mu);
@@ -244,16 +372,31 @@ struct l7m_batcher {
       l7m_ruleset_info info;
       l7m_ruleset_get_info(r, &info);
       int rc = dev_ok ? L7M_OK : L7M_EDEVICE;
-      if (rc == L7M_OK)
-        rc = info.proto == L7M_PROTO_KAFKA
-                 ? l7m_eval_device_ids(r, b->d_arena, bytes, b->d_offs, cnt, b->d_ids, b->d_verd, nullptr, stream, 0)
-                 : l7m_eval_device(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, nullptr, stream, 0);
-      const int64_t t_launch = now_ns();
-      if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
-      if (rc == L7M_OK) {
-        hipError_t q;
-        while ((q = hipEventQuery(ev)) == hipErrorNotReady) cpu_relax();
-        if (q != hipSuccess) rc = L7M_EDEVICE;
+      const uint32_t* dprog = nullptr;
+      int kind = 0;
+      uint32_t stage = 0;
+      uint64_t serial = 0;
+      int64_t t_launch;
+      bool normal = true;
+      if (rc == L7M_OK && res.ok && cnt <= kResidentMax &&
+          l7m::resident_program(r, &dprog, &kind, &stage, &serial)) {
+        t_launch = now_ns();
+        rc = resident_eval(r, dprog, kind, stage, serial, b, cnt, bytes);
+        normal = rc == 1;
+        if (normal) rc = L7M_OK;
+      }
+      if (normal) {
+        if (rc == L7M_OK)
+          rc = info.proto == L7M_PROTO_KAFKA
+                   ? l7m_eval_device_ids(r, b->d_arena, bytes, b->d_offs, cnt, b->d_ids, b->d_verd, nullptr, stream, 0)
+                   : l7m_eval_device(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, nullptr, stream, 0);
+        t_launch = now_ns();
+        if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
+        if (rc == L7M_OK) {
+          hipError_t q;
+          while ((q = hipEventQuery(ev)) == hipErrorNotReady) cpu_relax();
+          if (q != hipSuccess) rc = L7M_EDEVICE;
+        }
       }
       const int64_t t_done = now_ns();
       l7m_release(r);
@@ -389,6 +532,7 @@ int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batche
   b->cur.store(first);
   l7m_retain(rs);
   b->rs = rs;
+  b->resident_init();
   for (uint32_t i = 0; i < b->in_flight; ++i) b->flushers.emplace_back([b] { b->run(); });
   *out = b;
   return L7M_OK;
@@ -461,6 +605,7 @@ void l7m_batcher_destroy(l7m_batcher* b) {
   while (b->callers.load() != 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
   for (auto& t : b->flushers)
     if (t.joinable()) t.join();
+  b->resident_fini();
   l7m_release(b->rs);
   for (Batch* x : b->all) delete x;
   delete b;

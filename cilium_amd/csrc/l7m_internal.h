@@ -75,8 +75,14 @@ CompileResult compile_kafka_map(const l7m_kafka_selector_rules* map, size_t n_en
 
 // The opaque handle.  Immutable after compile except for the per-device
 // program copies, which are created lazily under `mu`.
+inline uint64_t next_ruleset_serial() {
+  static std::atomic<uint64_t> n{0};
+  return ++n;
+}
+
 struct l7m_ruleset {
   std::atomic<int> refs{1};
+  uint64_t serial = next_ruleset_serial();  // unique per handle (resident evaluator image cache key)
   uint32_t proto = 0;
   std::vector<uint32_t> program;
   l7m_ruleset_info info{};

@@ -622,14 +622,18 @@ enum KHitMode { kKNoHits = 0, kKLdsHits = 1, kKGlobalHits = 2 };
 // decoding; 2 = decode without table lookups.
 // kGroups: the program's rules belong to several L7DataMap entries, so each
 // request's source identity selects the rules that apply (else all do).
+// One workgroup's share (`part` of `nparts`) of a batch: the grid of
+// kafka_eval_kernel, or the single workgroup of kafka_resident_kernel, which
+// keeps the LDS tables of the previous batch when the program is the same
+// (load_tables false).
 template <int kHits, int kAblate, bool kCliLds, bool kGroups>
-__global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
-                                                             const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                             const uint64_t* __restrict__ offs, uint64_t n,
-                                                             int32_t* __restrict__ verdicts,
-                                                             unsigned long long* __restrict__ hits, uint32_t stage,
-                                                             uint32_t* __restrict__ crecs, uint32_t* qhdr,
-                                                             uint32_t qcap, const uint32_t* __restrict__ ids) {
+__device__ __forceinline__ void kafka_eval_body(const uint32_t* __restrict__ prog, const uint8_t* __restrict__ arena,
+                                                uint64_t arena_bytes, const uint64_t* __restrict__ offs, uint64_t n,
+                                                int32_t* __restrict__ verdicts,
+                                                unsigned long long* __restrict__ hits, uint32_t stage,
+                                                uint32_t* __restrict__ crecs, uint32_t* qhdr, uint32_t qcap,
+                                                const uint32_t* __restrict__ ids, bool load_tables, uint32_t part,
+                                                uint32_t nparts) {
   extern __shared__ __align__(16) uint32_t ksmem[];
   uint64_t prof[5] = {0, 0, 0, 0, 0};  // (kProf diagnostic builds)
   const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
@@ -645,14 +649,16 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   uint16_t* tq = reinterpret_cast<uint16_t*>(ctr + (kHits == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u));
   uint8_t* stg = reinterpret_cast<uint8_t*>(tq + kKWaves * 64 * kTopicQ) + wv * (stage + 16u);
   tq += wv * 64 * kTopicQ + lane;
-  if (kCliLds)
-    for (uint32_t i = tid; i < cli_words; i += kKBlock) cli[i] = prog[h.off_clients + i];
-  for (uint32_t i = tid; i < 2 * kKafkaKinds; i += kKBlock) ksmem[256 + kSpanLds + i] = prog[h.off_kind_ok + i];
-  for (uint32_t i = tid; i < 256; i += kKBlock) crc_tab[i] = prog[h.off_crc + i];
   static_assert(offsetof(KafkaHeader, all_by_kind) == offsetof(KafkaHeader, notopic_by_kind) + 8 * kKafkaKinds,
                 "span arrays are adjacent");
-  for (uint32_t i = tid; i < 4 * kKafkaKinds; i += kKBlock)
-    ksmem[256 + i] = prog[offsetof(KafkaHeader, notopic_by_kind) / 4 + i];
+  if (load_tables) {
+    if (kCliLds)
+      for (uint32_t i = tid; i < cli_words; i += kKBlock) cli[i] = prog[h.off_clients + i];
+    for (uint32_t i = tid; i < 2 * kKafkaKinds; i += kKBlock) ksmem[256 + kSpanLds + i] = prog[h.off_kind_ok + i];
+    for (uint32_t i = tid; i < 256; i += kKBlock) crc_tab[i] = prog[h.off_crc + i];
+    for (uint32_t i = tid; i < 4 * kKafkaKinds; i += kKBlock)
+      ksmem[256 + i] = prog[offsetof(KafkaHeader, notopic_by_kind) / 4 + i];
+  }
   if (kHits == kKLdsHits)
     for (uint32_t i = tid; i < n_ctr; i += kKBlock) ctr[i] = 0;
   __syncthreads();
@@ -668,8 +674,8 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
   v.strings = reinterpret_cast<const uint8_t*>(prog + h.off_strings);
   v.n_slots = kAblate == 2 ? 0 : h.n_slots;
 
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kKWaves + wv;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kKWaves;
+  const uint64_t gw = static_cast<uint64_t>(part) * kKWaves + wv;
+  const uint64_t nw = static_cast<uint64_t>(nparts) * kKWaves;
   const uint64_t end = n * (gw + 1) / nw;
   struct Tile {
     uint64_t cur, o, onext, base;
@@ -792,7 +798,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     wave_sync();  // the stage is overwritten by the next tile
     t = t2;
   }
-  if (kProf && blockIdx.x == 0 && wv == 0) {
+  if (kProf && part == 0 && wv == 0) {
     for (int k = 0; k < 5; ++k)
       for (uint32_t m = 1; m < 64; m <<= 1) {
         const uint64_t o2 = shfl64(prof[k], lane ^ m);
@@ -806,6 +812,83 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
     __syncthreads();
     for (uint32_t i = tid; i < n_ctr; i += kKBlock)
       if (ctr[i]) atomicAdd(hits + i, static_cast<unsigned long long>(ctr[i]));
+  }
+}
+
+template <int kHits, int kAblate, bool kCliLds, bool kGroups>
+__global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __restrict__ prog,
+                                                             const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                             const uint64_t* __restrict__ offs, uint64_t n,
+                                                             int32_t* __restrict__ verdicts,
+                                                             unsigned long long* __restrict__ hits, uint32_t stage,
+                                                             uint32_t* __restrict__ crecs, uint32_t* qhdr,
+                                                             uint32_t qcap, const uint32_t* __restrict__ ids) {
+  kafka_eval_body<kHits, kAblate, kCliLds, kGroups>(prog, arena, arena_bytes, offs, n, verdicts, hits, stage, crecs,
+                                                    qhdr, qcap, ids, true, blockIdx.x, gridDim.x);
+}
+
+__device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {  // uniform: in SGPRs
+  const uint64_t v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Resident Kafka evaluator: the mailbox protocol of http_resident_kernel
+// (l7m_kernels.hip), one workgroup.  Requests with compressed message sets
+// need the codec pass (kafka_codec_kernel): the resident workgroup has no
+// queue (capacity 0), counts them, and reports the batch back (slot.result
+// = 1) so the host evaluates that batch with the normal launches.
+template <bool kCliLds, bool kGroups>
+__global__ __launch_bounds__(kKBlock) void kafka_resident_kernel(ResidentBox* box, uint64_t seq, uint32_t* qhdr) {
+  extern __shared__ __align__(16) uint32_t ksmem[];
+  const uint32_t tid = threadIdx.x;
+  uint64_t* bc = reinterpret_cast<uint64_t*>(ksmem + kKLdsBytes / 4 - kResidentLdsWords);
+  const uint32_t* cur = nullptr;
+  uint64_t cur_gen = 0;
+  const uint64_t my_kind = kResidentKafka | (kCliLds ? 1u : 0u) | (kGroups ? 2u : 0u);
+  for (;;) {
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t act = 0;
+      for (;;) {
+        if (resident_load(&box->post_seq) >= seq) {
+          act = 1;
+          break;
+        }
+        if (resident_load(&box->quit) || __builtin_amdgcn_s_memrealtime() - t0 > kResidentIdleTicks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      bc[0] = act;
+    }
+    __syncthreads();
+    const uint64_t act = bc[0];
+    __syncthreads();
+    if (!act) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    ResidentSlot* sl = &box->slots[seq % kResidentSlots];
+    if (resident_load(&sl->kind) != my_kind) return;  // another instantiation: the host relaunches
+    const uint64_t gen = resident_load(&sl->gen);
+    const uint32_t* prog = reinterpret_cast<const uint32_t*>(resident_load(&sl->prog));
+    const uint8_t* arena = reinterpret_cast<const uint8_t*>(resident_load(&sl->arena));
+    const uint64_t* offs = reinterpret_cast<const uint64_t*>(resident_load(&sl->offs));
+    int32_t* verdicts = reinterpret_cast<int32_t*>(resident_load(&sl->verdicts));
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(resident_load(&sl->ids));
+    const uint64_t arena_bytes = resident_load(&sl->arena_bytes), n = resident_load(&sl->n);
+    const uint32_t stage = static_cast<uint32_t>(resident_load(&sl->stage));
+    kafka_eval_body<kKNoHits, 0, kCliLds, kGroups>(prog, arena, arena_bytes, offs, n, verdicts, nullptr, stage,
+                                                   nullptr, qhdr, 0, ids, prog != cur || gen != cur_gen, 0, 1);
+    cur = prog;
+    cur_gen = gen;
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t queued = __hip_atomic_load(qhdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(qhdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sl->result, queued ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->done_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    ++seq;
   }
 }
 
@@ -823,6 +906,48 @@ static hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const uint
 
 }  // namespace
 
+// Record stage of a Kafka workgroup (what the LDS leaves after the tables),
+// `reserve` bytes kept at the end.
+static size_t kafka_stage(const KafkaHeader& h, int mode, bool cli_lds, size_t reserve) {
+  const uint32_t n_ctr = h.n_rules + 2;
+  const size_t cli_words = static_cast<size_t>(h.n_clients) * (sizeof(KafkaClientSlot) / 4);
+  const size_t fixed = 4u * (256u + kSpanLds + kKindOkLds + (cli_lds ? cli_words : 0u) +
+                             (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
+                       2u * kKWaves * 64 * kTopicQ;
+  size_t stage = (kKLdsBytes - reserve - fixed) / kKWaves - 16u;
+  stage &= ~size_t(15);
+  return stage > kKMaxStage ? kKMaxStage : stage;
+}
+
+bool kafka_resident_ok(const KafkaHeader& h, int* kind, uint32_t* stage) {
+  const size_t cli_words = static_cast<size_t>(h.n_clients) * (sizeof(KafkaClientSlot) / 4);
+  const bool cli_lds = cli_words && cli_words * 4 <= kMaxCliLdsBytes;
+  const size_t st = kafka_stage(h, kKNoHits, cli_lds, 4u * kResidentLdsWords);
+  if (st < 1024) return false;
+  *kind = static_cast<int>(kResidentKafka | (cli_lds ? 1u : 0u) | (h.n_id_slots ? 2u : 0u));
+  *stage = static_cast<uint32_t>(st);
+  return true;
+}
+
+hipError_t launch_kafka_resident(ResidentBox* dbox, uint64_t first_seq, int kind, uint32_t* qhdr,
+                                 hipStream_t stream) {
+#define L7M_KRES(C, G)                                                                                        \
+  {                                                                                                          \
+    const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(kafka_resident_kernel<C, G>), kKLdsBytes); \
+    if (e != hipSuccess) return e;                                                                           \
+    hipLaunchKernelGGL((kafka_resident_kernel<C, G>), dim3(1), dim3(kKBlock), kKLdsBytes, stream, dbox, first_seq, \
+                       qhdr);                                                                                \
+    return hipGetLastError();                                                                                \
+  }
+  switch (kind & 3) {
+    case 0: L7M_KRES(false, false)
+    case 1: L7M_KRES(true, false)
+    case 2: L7M_KRES(false, true)
+    default: L7M_KRES(true, true)
+  }
+#undef L7M_KRES
+}
+
 hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                         const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
                         hipStream_t stream, int num_cus, uint32_t flags, const KafkaCodecQueue& cq,
@@ -835,9 +960,7 @@ hipError_t launch_kafka(const uint32_t* dprog, const KafkaHeader& h, const uint8
   const size_t fixed = 4u * (256u + kSpanLds + kKindOkLds + (cli_lds ? cli_words : 0u) +
                              (mode == kKLdsHits ? ((n_ctr + 3u) & ~3u) : 0u)) +
                        2u * kKWaves * 64 * kTopicQ;
-  size_t stage = (kKLdsBytes - fixed) / kKWaves - 16u;
-  stage &= ~size_t(15);
-  if (stage > kKMaxStage) stage = kKMaxStage;
+  const size_t stage = kafka_stage(h, mode, cli_lds, 0);
   const size_t lds = fixed + kKWaves * (stage + 16u);
   uint64_t blocks = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256);
   const uint64_t want = (n + 2 * kKBlock - 1) / (2 * kKBlock);

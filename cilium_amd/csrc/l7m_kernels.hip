@@ -469,6 +469,43 @@ __device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd,
   return acc | gld(c.prog + dd.es_off + st);
 }
 
+// Up to four search automata (consecutive DFAs d0 .. d0 + m - 1 of one
+// field) over the same bytes, interleaved: their table reads are independent,
+// so m L2 round trips are in flight per byte instead of one (config 2 in the
+// RE2 dialect walks ~32 automata per path).
+template <class Src>
+__device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t m, const Src& src, uint32_t pos,
+                                             uint32_t len, uint32_t (&out)[4]) {
+  const uint32_t* T[4];
+  const uint8_t* cm[4];
+  const uint32_t* mid[4];
+  uint32_t ncls[4], st[4], acc[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const DfaDesc& dd = c.dds[d0 + (j < m ? j : 0u)];
+    T[j] = c.prog + dd.table_off;
+    cm[j] = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
+    mid[j] = c.prog + dd.acc_mid_off;
+    ncls[j] = dd.acc_ncls;
+    st[j] = dd.start_base;
+    acc[j] = dd.start_es8;
+  }
+  for (uint32_t k = 0; k < len; ++k) {
+    const uint32_t b = src.byte(pos + k);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      if (j < m) {
+        const uint32_t e = gld(T[j] + st[j] * ncls[j] + cm[j][b]);
+        st[j] = e & 0xffffffu;
+        acc[j] |= gld(mid[j] + (e >> 24));
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j)
+    out[j] = j < m ? acc[j] | gld(c.prog + c.dds[d0 + j].es_off + st[j]) : 0u;
+}
+
 template <bool kLit, bool kSearch, class Src>
 __device__ __forceinline__ uint32_t walk_dfa(const Ctx& c, uint32_t d, const Src& src, uint32_t pos, uint32_t len) {
   const DfaDesc& dd = c.dds[d];
@@ -547,6 +584,12 @@ __device__ __forceinline__ uint32_t ent_lookup(const Ctx& c, const HttpHeader& h
     if (k == key + 1) return lds ? lld(tab + 2 * at + 1) : gld(tab + 2 * at + 1);
   }
 }
+
+#ifndef L7M_MIN_STAGED
+#define L7M_MIN_STAGED 32
+#endif
+constexpr uint32_t kMinStagedTake = L7M_MIN_STAGED;
+static_assert(kMinStagedTake >= 1, "a tile takes at least one record");
 
 // Diagnostic timeline (L7M_PROF builds, kProf): per-lane cycle accumulators
 // per evaluation phase (s_memtime), LDS-staged records only; prof[0] = last
@@ -732,6 +775,19 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
       const FieldDesc& fd = c.fields[f];
       for (uint32_t k = 0; k < fd.ndfa; ++k) {
         const uint32_t d = fd.dfa_first + k;
+        if constexpr (kReg < 0) {
+          if (c.dds[d].kind == kDfaSearch) {  // a run of search automata, four at a time
+            uint32_t m = 1;
+            while (m < 4 && k + m < fd.ndfa && c.dds[d + m].kind == kDfaSearch) ++m;
+            uint32_t out[4];
+            walk_search4(c, d, m, src, p, len, out);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+              if (j < m) codes.set(d + j, out[j]);
+            k += m - 1;
+            continue;
+          }
+        }
         const uint32_t code = walk_dfa<kLit, (kReg < 0)>(c, d, src, p, len);
         HPROF(3);  // the walk, end code included
         codes.set(d, code);
@@ -999,13 +1055,17 @@ enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
 #else
 #define L7M_HTTP_OCC
 #endif
+// The evaluation of one batch by one workgroup, `part` of `nparts` (the
+// grid of http_eval_kernel, or the single workgroup of http_resident_kernel,
+// which keeps the LDS image of the previous batch when the program is the
+// same: load_image false).
 template <int kHits, int kReg, int kAblate, bool kLit>
-__global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const uint32_t* __restrict__ prog,
-                                                           const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                           const uint64_t* __restrict__ offs, uint64_t n,
-                                                           int32_t* __restrict__ verdicts,
-                                                           unsigned long long* __restrict__ hits, uint32_t stage,
-                                                           uint32_t* __restrict__ scratch, uint32_t* __restrict__ slowq) {
+__device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog, const uint8_t* __restrict__ arena,
+                                               uint64_t arena_bytes, const uint64_t* __restrict__ offs, uint64_t n,
+                                               int32_t* __restrict__ verdicts, unsigned long long* __restrict__ hits,
+                                               uint32_t stage, uint32_t* __restrict__ scratch,
+                                               uint32_t* __restrict__ slowq, bool load_image, uint32_t part,
+                                               uint32_t nparts) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -1014,13 +1074,13 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
   uint32_t* ctr = smem + h.lds_image_words;  // LDS hit counters (kLdsHits)
   uint32_t* col = ctr + (kHits == kLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);  // LDS code columns (!kReg)
   uint8_t* stg = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock)) + wv * (stage + 16u);
-  {
+  if (load_image) {
     const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
     uint4* l = reinterpret_cast<uint4*>(img);
     for (uint32_t i = tid; i < h.lds_image_words / 4u; i += kBlock) l[i] = g[i];
-    if (kHits == kLdsHits)
-      for (uint32_t i = tid; i < n_ctr; i += kBlock) ctr[i] = 0;
   }
+  if (kHits == kLdsHits)
+    for (uint32_t i = tid; i < n_ctr; i += kBlock) ctr[i] = 0;
   __syncthreads();
 
   Ctx c;
@@ -1052,8 +1112,8 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
   // This wave's contiguous share of the batch, consumed in tiles of <= 64
   // records.  Software pipeline per wave: while tile t is evaluated from the
   // LDS stage, tile t+1's bytes and tile t+2's offsets are already in flight.
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wv;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  const uint64_t gw = static_cast<uint64_t>(part) * kWaves + wv;
+  const uint64_t nw = static_cast<uint64_t>(nparts) * kWaves;
   const uint64_t end = n * (gw + 1) / nw;
   struct Tile {
     uint64_t cur, o, onext, base;
@@ -1086,7 +1146,10 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     const uint64_t okm = __ballot(ok);
     t.k = okm == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~okm));
     t.bytes = t.k ? static_cast<uint32_t>(readlane64(onext, t.k - 1) - t.base) : 0u;
-    t.take = t.k ? t.k : 1u;
+    // A stage that holds fewer than half a tile of records (large records,
+    // config 5: 7-12 of 64) would leave most lanes idle: the tile then takes
+    // all m records and lanes past the staged run read theirs from HBM.
+    t.take = t.k >= kMinStagedTake ? t.k : static_cast<uint32_t>(m);
     return t;
   };
   // Staging by LDS-DMA (global_load_lds_dwordx4, non-temporal): the next
@@ -1125,8 +1188,8 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     WalkOut<kReg> wo;
     if constexpr (!kReg) wo.codes.p = mycol;
     if constexpr (kReg < 0) {  // search programs: the codes live in the global scratch
-      wo.codes.p = scratch + static_cast<uint64_t>(blockIdx.x) * kBlock + tid;
-      wo.codes.stride = gridDim.x * kBlock;
+      wo.codes.p = scratch + static_cast<uint64_t>(part) * kBlock + tid;
+      wo.codes.stride = nparts * kBlock;
     }
     if (lane < take) {
       bool done = false;
@@ -1183,11 +1246,11 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     qtn(5);
     qt[6] += 1;
   }
-  if (kProf && ((blockIdx.x == 0 && wv == 0) || (blockIdx.x == 101 && wv == 7))) {
+  if (kProf && ((part == 0 && wv == 0) || (part == 101 && wv == 7))) {
     if (lane == 0)
       printf("L7M_QT block %u wave %u tiles %llu cycles/tile: topwait %llu walks %llu entry %llu issue %llu "
              "verify %llu counters %llu\n",
-             blockIdx.x, wv, (unsigned long long)qt[6], (unsigned long long)(qt[0] / (qt[6] ? qt[6] : 1)),
+             part, wv, (unsigned long long)qt[6], (unsigned long long)(qt[0] / (qt[6] ? qt[6] : 1)),
              (unsigned long long)(qt[1] / (qt[6] ? qt[6] : 1)), (unsigned long long)(qt[2] / (qt[6] ? qt[6] : 1)),
              (unsigned long long)(qt[3] / (qt[6] ? qt[6] : 1)), (unsigned long long)(qt[4] / (qt[6] ? qt[6] : 1)),
              (unsigned long long)(qt[5] / (qt[6] ? qt[6] : 1)));
@@ -1207,6 +1270,83 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
     __syncthreads();
     for (uint32_t i = tid; i < n_ctr; i += kBlock)
       if (ctr[i]) atomicAdd(hits + i, static_cast<unsigned long long>(ctr[i]));
+  }
+}
+
+template <int kHits, int kReg, int kAblate, bool kLit>
+__global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const uint32_t* __restrict__ prog,
+                                                           const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                           const uint64_t* __restrict__ offs, uint64_t n,
+                                                           int32_t* __restrict__ verdicts,
+                                                           unsigned long long* __restrict__ hits, uint32_t stage,
+                                                           uint32_t* __restrict__ scratch, uint32_t* __restrict__ slowq) {
+  http_eval_body<kHits, kReg, kAblate, kLit>(prog, arena, arena_bytes, offs, n, verdicts, hits, stage, scratch, slowq,
+                                             true, blockIdx.x, gridDim.x);
+}
+
+// Resident evaluator for small batches (the batcher's per-request latency
+// path, l7m_batch.cc): ONE workgroup stays on the GPU and polls a mailbox in
+// pinned host memory (ResidentBox, l7m_device.h) for posted batches, so a
+// batch costs no kernel launch, no completion signal and no LDS image load
+// (the image is kept while the program is the same).  Per batch: wait until
+// post_seq reaches the next sequence number, read its slot, evaluate it with
+// the http_eval_kernel code (records and verdicts in pinned host memory),
+// publish done_seq.  Exit (every wave takes the same branch after a barrier):
+// quit set by the host, a slot for another instantiation (the host relaunches
+// the right one), or kResidentIdleTicks of s_memrealtime (100 MHz) without
+// work, so the workgroup drains by itself when its process ends.
+// (a uniform value: moved to SGPRs, so the program header is read with
+// scalar loads as in http_eval_kernel; the host keeps every program it posts
+// alive until the instance ends, so no cached line goes stale)
+__device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
+  const uint64_t v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+template <int kReg>
+__global__ __launch_bounds__(kBlock) void http_resident_kernel(ResidentBox* box, uint64_t seq) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  const uint32_t tid = threadIdx.x;
+  uint64_t* bc = reinterpret_cast<uint64_t*>(smem + kHttpLdsBytes / 4 - kResidentLdsWords);  // broadcast
+  const uint32_t* cur = nullptr;
+  uint64_t cur_gen = 0;
+  for (;;) {
+    if (tid == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t act = 0;
+      for (;;) {
+        if (resident_load(&box->post_seq) >= seq) {
+          act = 1;
+          break;
+        }
+        if (resident_load(&box->quit) || __builtin_amdgcn_s_memrealtime() - t0 > kResidentIdleTicks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      bc[0] = act;
+    }
+    __syncthreads();
+    const uint64_t act = bc[0];
+    __syncthreads();
+    if (!act) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // slot fields and records written before post_seq
+    const ResidentSlot* sl = &box->slots[seq % kResidentSlots];
+    const uint64_t kind = resident_load(&sl->kind), gen = resident_load(&sl->gen);
+    if (kind != static_cast<uint64_t>(kReg)) return;  // another instantiation: the host relaunches
+    const uint32_t* prog = reinterpret_cast<const uint32_t*>(resident_load(&sl->prog));
+    const uint8_t* arena = reinterpret_cast<const uint8_t*>(resident_load(&sl->arena));
+    const uint64_t* offs = reinterpret_cast<const uint64_t*>(resident_load(&sl->offs));
+    int32_t* verdicts = reinterpret_cast<int32_t*>(resident_load(&sl->verdicts));
+    const uint64_t arena_bytes = resident_load(&sl->arena_bytes), n = resident_load(&sl->n);
+    const uint32_t stage = static_cast<uint32_t>(resident_load(&sl->stage));
+    http_eval_body<kNoHits, kReg, 0, false>(prog, arena, arena_bytes, offs, n, verdicts, nullptr, stage, nullptr,
+                                            nullptr, prog != cur || gen != cur_gen, 0, 1);
+    cur = prog;
+    cur_gen = gen;
+    __threadfence_system();  // this thread's verdict stores before done_seq
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&box->done_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    ++seq;
   }
 }
 
@@ -1307,6 +1447,37 @@ static hipError_t launch_slow(const HttpHeader& h, hipStream_t stream, const uin
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_slow_kernel<kReg, kLit>), dim3(kSlowBlocks), dim3(kBlock), lds, stream, dprog, arena,
                      arena_bytes, offs, n, verdicts, hits, slowq, vmscratch);
+  return hipGetLastError();
+}
+
+bool http_resident_ok(const HttpHeader& h, uint32_t flags, int* kind, uint32_t* stage) {
+  if (h.search || h.n_slow || (flags & kLaunchLiterals) || h.n_dfas > kRegDfas) return false;
+  const uint32_t s = http_stage_bytes(h);
+  if (s == 0) return false;
+  // the resident workgroup keeps kResidentLdsWords at the end of the LDS
+  uint32_t st = s;
+  while (st > 256 && http_lds_bytes(h, st) + 4u * kResidentLdsWords > kHttpLdsBytes) st -= 16;
+  if (http_lds_bytes(h, st) + 4u * kResidentLdsWords > kHttpLdsBytes) return false;
+  *kind = h.n_dfas <= 4 ? 4 : 8;
+  *stage = st;
+  return true;
+}
+
+hipError_t launch_resident(ResidentBox* dbox, uint64_t first_seq, int kind, uint32_t* qhdr, hipStream_t stream) {
+  if (static_cast<uint64_t>(kind) & kResidentKafka) return launch_kafka_resident(dbox, first_seq, kind, qhdr, stream);
+  return launch_http_resident(dbox, first_seq, kind, stream);
+}
+
+hipError_t launch_http_resident(ResidentBox* dbox, uint64_t first_seq, int kind, hipStream_t stream) {
+  if (kind == 4) {
+    const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_resident_kernel<4>), kHttpLdsBytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(http_resident_kernel<4>, dim3(1), dim3(kBlock), kHttpLdsBytes, stream, dbox, first_seq);
+  } else {
+    const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_resident_kernel<8>), kHttpLdsBytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(http_resident_kernel<8>, dim3(1), dim3(kBlock), kHttpLdsBytes, stream, dbox, first_seq);
+  }
   return hipGetLastError();
 }
 

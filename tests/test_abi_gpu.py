@@ -116,3 +116,62 @@ def test_batcher_destroy_with_calls_in_flight(gpu):
         with pytest.raises(L.L7Error) as e:
             b.eval(recs[0])
         assert e.value.code == L.L7M_EINVAL
+
+
+def test_batcher_resident_evaluator_relaunch_and_rule_switch(gpu):
+    """The batcher's resident HTTP evaluator (one workgroup polling a pinned
+    mailbox, l7m_kernels.hip http_resident_kernel): verdicts equal the
+    oracle's across its idle exit and relaunch (> 20 ms without batches), a
+    switch to a program of the other instantiation (7 value DFAs: 8-register
+    end codes), to one it cannot serve (back-references: slow path, normal
+    launches) and back, with 8 threads calling concurrently."""
+    import threading
+    import time
+    import numpy as np
+    from regex_ext_cases import REALISTIC, realistic_requests
+
+    rng = np.random.default_rng(5)
+    rules_a = W.rules(2)
+    arena, offs = W.requests(2, 13_000_000, 400)
+    recs_a = [arena[int(offs[i]):int(offs[i + 1]) if i + 1 < len(offs) else arena.nbytes - 64].tobytes()
+              for i in range(len(offs))]
+    exp_a = HttpOracle(rules_a).eval(arena, offs, threads=8)
+    rules_b = [L.PortRuleHTTP(Path="/a/.*", Method="GET", Host="h[0-9]+\\.example",
+                              Headers=["X-A: 1", "X-B: two", "X-C: 3"]),
+               L.PortRuleHTTP(Path="/b/[a-z]+", Method="POST", Headers=["X-D: 4"])]
+    reqs_b = []
+    for i in range(300):
+        hdr = [("x-a", "1"), ("x-b", "two"), ("x-c", "3")] if rng.random() < 0.7 else [("x-d", "4")]
+        reqs_b.append(L.HTTPRequest(str(rng.choice(["GET", "POST"])), str(rng.choice(["/a/x", "/b/yz", "/b/9", "/c"])),
+                                    str(rng.choice(["h1.example", "h22.example", "hx.example"])), hdr))
+    ab, ob = L.pack_http(reqs_b)
+    recs_b = [ab[int(ob[i]):int(ob[i + 1]) if i + 1 < len(ob) else ab.nbytes - 64].tobytes() for i in range(len(ob))]
+    exp_b = HttpOracle(rules_b).eval(ab, ob)
+    ac, oc = L.pack_http(realistic_requests(rng, 300))
+    recs_c = [ac[int(oc[i]):int(oc[i + 1]) if i + 1 < len(oc) else ac.nbytes - 64].tobytes() for i in range(len(oc))]
+    exp_c = HttpOracle(REALISTIC).eval(ac, oc)
+
+    rs_a, rs_b, rs_c = (L.RuleSet.compile_http(r) for r in (rules_a, rules_b, REALISTIC))
+    b = L.Batcher(rs_a, max_delay_us=100, in_flight=3)
+
+    def run(recs, exp):
+        got = np.full(len(recs), -100, dtype=np.int64)
+
+        def worker(t):
+            for i in range(t, len(recs), 8):
+                got[i] = b.eval(recs[i])
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert np.array_equal(got, exp)
+
+    run(recs_a, exp_a)
+    time.sleep(0.06)  # the resident workgroup exits after 20 ms idle
+    run(recs_a, exp_a)
+    for rs, recs, exp in ((rs_b, recs_b, exp_b), (rs_c, recs_c, exp_c), (rs_a, recs_a, exp_a), (rs_b, recs_b, exp_b)):
+        b.set_ruleset(rs)
+        run(recs, exp)
+    b.close()

@@ -90,3 +90,31 @@ def test_random_multi_partition_produce_requests_gpu(gpu):
     recs = C.random_produce_requests(random.Random(23), 3000, framing_stops=True)
     v = _check([L.PortRuleKafka(Topic="t")], recs)
     assert (v == 0).any() and (v == -1).any() and (v == -2).any()
+
+
+def test_batcher_resident_kafka_codec_fallback(gpu):
+    """Through the batcher, Kafka batches go to the resident workgroup; a
+    batch holding a compressed message set is handed back (the resident
+    workgroup has no codec queue) and evaluated by the normal launches with
+    the second pass: verdicts equal the oracle's for a mix of plain and
+    compressed / corrupt produce requests called from 8 threads."""
+    import threading
+    recs = C.random_produce_requests(random.Random(29), 600, framing_stops=True)
+    rules = [L.PortRuleKafka(Topic="t")]
+    arena, offs = L.pack_records(recs)
+    exp = KafkaOracle(rules).eval(arena, offs)
+    b = L.Batcher(L.RuleSet.compile_kafka(rules), max_delay_us=100, in_flight=3)
+    got = np.full(len(recs), -100, dtype=np.int64)
+
+    def worker(t):
+        for i in range(t, len(recs), 8):
+            got[i] = b.eval(recs[i])
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    b.close()
+    assert np.array_equal(got, exp)
+    assert (exp == -2).any() and (exp == 0).any()
