@@ -158,6 +158,7 @@ struct l7m_batcher {
   std::vector<std::thread> flushers;
   // statistics (l7m_batcher_stats / l7m_batcher_get_profile)
   std::atomic<uint64_t> batches{0}, requests{0}, fill_ns{0}, launch_ns{0}, gpu_ns{0}, wake_ns{0};
+  std::atomic<uint64_t> res_batches{0}, res_read{0}, res_eval{0}, res_sync{0};  // device ticks (100 MHz)
 
   // Resident evaluator (l7m_kernels.hip http_resident_kernel): batches of
   // up to kResidentMax HTTP records whose program it can serve are posted to
@@ -187,7 +188,8 @@ struct l7m_batcher {
   void resident_init() {
     (void)hipSetDevice(device);
     void* p = nullptr;
-    if (hipHostMalloc(&p, sizeof(l7m::ResidentBox), hipHostMallocMapped) != hipSuccess || !p) return;
+    if (hipHostMalloc(&p, sizeof(l7m::ResidentBox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !p)
+      return;
     std::memset(p, 0, sizeof(l7m::ResidentBox));
     res.box = static_cast<l7m::ResidentBox*>(p);
     void* d = nullptr;
@@ -266,7 +268,16 @@ struct l7m_batcher {
     // L7M_OK, or 1: the workgroup asks for the normal launches (Kafka
     // batches with compressed message sets need the codec pass)
     auto outcome = [&]() -> int {
-      return __atomic_load_n(&res.box->slots[seq % l7m::kResidentSlots].result, __ATOMIC_ACQUIRE) ? 1 : L7M_OK;
+      const l7m::ResidentSlot& sl = res.box->slots[seq % l7m::kResidentSlots];
+      uint64_t st[4];
+      for (int k = 0; k < 4; ++k) st[k] = __atomic_load_n(&sl.stamp[k], __ATOMIC_ACQUIRE);
+      if (st[3] >= st[2] && st[2] >= st[1] && st[1] >= st[0]) {
+        res_batches.fetch_add(1);
+        res_read.fetch_add(st[1] - st[0]);
+        res_eval.fetch_add(st[2] - st[1]);
+        res_sync.fetch_add(st[3] - st[2]);
+      }
+      return __atomic_load_n(&sl.result, __ATOMIC_ACQUIRE) ? 1 : L7M_OK;
     };
     for (uint32_t spin = 0;; ++spin) {
       if (__atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= seq) return outcome();
@@ -586,6 +597,11 @@ int l7m_batcher_get_profile(l7m_batcher* b, l7m_batcher_profile* out) {
   out->fill_us = nb ? b->fill_ns.load() / 1e3 / nb : 0.0;
   out->launch_us = nb ? b->launch_ns.load() / 1e3 / nb : 0.0;
   out->gpu_us = nb ? b->gpu_ns.load() / 1e3 / nb : 0.0;
+  const uint64_t rb = b->res_batches.load();
+  out->resident_batches = rb;
+  out->resident_read_us = rb ? b->res_read.load() / 100.0 / rb : 0.0;  // 100 ticks per us
+  out->resident_eval_us = rb ? b->res_eval.load() / 100.0 / rb : 0.0;
+  out->resident_sync_us = rb ? b->res_sync.load() / 100.0 / rb : 0.0;
   out->wake_us = nr ? b->wake_ns.load() / 1e3 / nr : 0.0;
   return L7M_OK;
 }

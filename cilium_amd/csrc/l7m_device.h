@@ -47,7 +47,7 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
 // evaluates the slot and raises done_seq to seq.  Every field is read and
 // written with system-scope atomics.
 constexpr uint32_t kResidentSlots = 16;
-constexpr uint32_t kResidentLdsWords = 4;  // broadcast words at the end of the resident workgroup's LDS
+constexpr uint32_t kResidentLdsWords = 40;  // broadcast words (decision + slot copy) at the end of the resident LDS
 constexpr uint64_t kResidentIdleTicks = 2000000;  // 20 ms of s_memrealtime (100 MHz) without work: exit
 constexpr uint64_t kResidentKafka = 16;          // kind of a Kafka slot: kResidentKafka | cli_lds | groups << 1
 struct ResidentSlot {
@@ -55,8 +55,12 @@ struct ResidentSlot {
   uint64_t gen;   // program generation (a new program at a reused address reloads the image)
   uint64_t prog, arena, arena_bytes, offs, n, verdicts, stage, ids;
   uint64_t result;  // written by the workgroup: 1 = evaluate this batch again with the normal launches
-  uint64_t pad[5];
+  // written by the workgroup (s_memrealtime, 100 MHz): batch seen, slot read
+  // and caches invalidated, batch evaluated, verdicts written back
+  uint64_t stamp[4];
+  uint64_t pad;
 };
+static_assert(sizeof(ResidentSlot) == 128, "the resident workgroup reads a slot as 16 words");
 struct ResidentBox {
   alignas(64) uint64_t post_seq;
   alignas(64) uint64_t done_seq;

@@ -827,11 +827,13 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
                                                     qhdr, qcap, ids, true, blockIdx.x, gridDim.x);
 }
 
-__device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {  // uniform: in SGPRs
-  const uint64_t v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {  // uniform: in SGPRs
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
   return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
+  return uniform64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 
 // Resident Kafka evaluator: the mailbox protocol of http_resident_kernel
@@ -860,33 +862,46 @@ __global__ __launch_bounds__(kKBlock) void kafka_resident_kernel(ResidentBox* bo
         __builtin_amdgcn_s_sleep(1);
       }
       bc[0] = act;
+      bc[1] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const uint64_t act = bc[0];
     __syncthreads();
     if (!act) return;
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    ResidentSlot* sl = &box->slots[seq % kResidentSlots];
-    if (resident_load(&sl->kind) != my_kind) return;  // another instantiation: the host relaunches
-    const uint64_t gen = resident_load(&sl->gen);
-    const uint32_t* prog = reinterpret_cast<const uint32_t*>(resident_load(&sl->prog));
-    const uint8_t* arena = reinterpret_cast<const uint8_t*>(resident_load(&sl->arena));
-    const uint64_t* offs = reinterpret_cast<const uint64_t*>(resident_load(&sl->offs));
-    int32_t* verdicts = reinterpret_cast<int32_t*>(resident_load(&sl->verdicts));
-    const uint32_t* ids = reinterpret_cast<const uint32_t*>(resident_load(&sl->ids));
-    const uint64_t arena_bytes = resident_load(&sl->arena_bytes), n = resident_load(&sl->n);
-    const uint32_t stage = static_cast<uint32_t>(resident_load(&sl->stage));
+    if (tid == 0) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // one L1 / L2 invalidation per batch
+    ResidentSlot* slp = &box->slots[seq % kResidentSlots];
+    if (tid < 16)  // the slot in one round trip
+      bc[2 + tid] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(slp) + tid, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    const ResidentSlot sl = *reinterpret_cast<const ResidentSlot*>(bc + 2);
+    if (uniform64(sl.kind) != my_kind) return;  // another instantiation: the host relaunches
+    const uint64_t gen = uniform64(sl.gen);
+    const uint32_t* prog = reinterpret_cast<const uint32_t*>(uniform64(sl.prog));
+    const uint8_t* arena = reinterpret_cast<const uint8_t*>(uniform64(sl.arena));
+    const uint64_t* offs = reinterpret_cast<const uint64_t*>(uniform64(sl.offs));
+    int32_t* verdicts = reinterpret_cast<int32_t*>(uniform64(sl.verdicts));
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(uniform64(sl.ids));
+    const uint64_t arena_bytes = uniform64(sl.arena_bytes), n = uniform64(sl.n);
+    const uint32_t stage = static_cast<uint32_t>(uniform64(sl.stage));
+    const uint64_t t_read = __builtin_amdgcn_s_memrealtime();
     kafka_eval_body<kKNoHits, 0, kCliLds, kGroups>(prog, arena, arena_bytes, offs, n, verdicts, nullptr, stage,
                                                    nullptr, qhdr, 0, ids, prog != cur || gen != cur_gen, 0, 1);
     cur = prog;
     cur_gen = gen;
-    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+      const uint64_t t_body = __builtin_amdgcn_s_memrealtime();
+      __threadfence_system();  // one L2 write-back per batch: the verdicts, then done_seq
+      const uint64_t t_sync = __builtin_amdgcn_s_memrealtime();
+      const uint64_t st[4] = {bc[1], t_read, t_body, t_sync};
+      for (int k = 0; k < 4; ++k)
+        __hip_atomic_store(&slp->stamp[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const uint32_t queued = __hip_atomic_load(qhdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(qhdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sl->result, queued ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&box->done_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&slp->result, queued ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->done_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     ++seq;
   }

@@ -68,18 +68,14 @@ struct LdsSrc {
   const uint32_t* w;  // word 0 of the record in the wave's LDS stage
   __device__ __forceinline__ uint32_t word(uint32_t i) const { return w[i]; }
   __device__ __forceinline__ uint32_t byte(uint32_t i) const { return reinterpret_cast<const uint8_t*>(w)[i]; }
-#ifdef L7M_ALIGNED_WORDS
-  // bytes [p, p + 4) from two 4-byte-aligned reads (a b64 read off its 8-byte
-  // alignment is replayed by the LDS)
+  // bytes [p, p + 4) from 4-byte-aligned reads and v_alignbyte: the byte
+  // reads would be merged into a b64 read off its 8-byte alignment, which the
+  // LDS replays (SQ_LDS_UNALIGNED_STALL 32 % of LDS-active cycles on config
+  // 2; measured 3.516 vs 3.566 ms, profiles/r04/ab_round4.md)
   __device__ __forceinline__ uint32_t word_u(uint32_t p) const {
     const uint32_t* a = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(w) + (p & ~3u));
     return __builtin_amdgcn_alignbyte(a[1], a[0], p & 3u);
   }
-#else
-  __device__ __forceinline__ uint32_t word_u(uint32_t p) const {
-    return byte(p) | byte(p + 1) << 8 | byte(p + 2) << 16 | byte(p + 3) << 24;
-  }
-#endif
 };
 struct GlbSrc {
   static constexpr bool kLds = false;
@@ -585,11 +581,7 @@ __device__ __forceinline__ uint32_t ent_lookup(const Ctx& c, const HttpHeader& h
   }
 }
 
-#ifndef L7M_MIN_STAGED
-#define L7M_MIN_STAGED 32
-#endif
-constexpr uint32_t kMinStagedTake = L7M_MIN_STAGED;
-static_assert(kMinStagedTake >= 1, "a tile takes at least one record");
+constexpr uint32_t kMinStagedTake = 32;
 
 // Diagnostic timeline (L7M_PROF builds, kProf): per-lane cycle accumulators
 // per evaluation phase (s_memtime), LDS-staged records only; prof[0] = last
@@ -1295,14 +1287,23 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
 // quit set by the host, a slot for another instantiation (the host relaunches
 // the right one), or kResidentIdleTicks of s_memrealtime (100 MHz) without
 // work, so the workgroup drains by itself when its process ends.
+// Memory model: mailbox fields are read and written with relaxed
+// system-scope atomics (they bypass the caches); per batch ONE thread
+// invalidates the CU's L1 and the L2 before the records are read and ONE
+// thread writes the L2 back after every thread's verdict stores have been
+// acknowledged (s_waitcnt vmcnt(0) + barrier), then stores done_seq.
+// (Acquire / release fences in every thread and every mailbox read cost
+// ~200 us per batch: measured, gpurun_out/r04f.)
 // (a uniform value: moved to SGPRs, so the program header is read with
 // scalar loads as in http_eval_kernel; the host keeps every program it posts
 // alive until the instance ends, so no cached line goes stale)
-__device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
-  const uint64_t v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
   return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
+  return uniform64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 template <int kReg>
 __global__ __launch_bounds__(kBlock) void http_resident_kernel(ResidentBox* box, uint64_t seq) {
@@ -1324,28 +1325,44 @@ __global__ __launch_bounds__(kBlock) void http_resident_kernel(ResidentBox* box,
         __builtin_amdgcn_s_sleep(1);
       }
       bc[0] = act;
+      bc[1] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const uint64_t act = bc[0];
     __syncthreads();
     if (!act) return;
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // slot fields and records written before post_seq
-    const ResidentSlot* sl = &box->slots[seq % kResidentSlots];
-    const uint64_t kind = resident_load(&sl->kind), gen = resident_load(&sl->gen);
-    if (kind != static_cast<uint64_t>(kReg)) return;  // another instantiation: the host relaunches
-    const uint32_t* prog = reinterpret_cast<const uint32_t*>(resident_load(&sl->prog));
-    const uint8_t* arena = reinterpret_cast<const uint8_t*>(resident_load(&sl->arena));
-    const uint64_t* offs = reinterpret_cast<const uint64_t*>(resident_load(&sl->offs));
-    int32_t* verdicts = reinterpret_cast<int32_t*>(resident_load(&sl->verdicts));
-    const uint64_t arena_bytes = resident_load(&sl->arena_bytes), n = resident_load(&sl->n);
-    const uint32_t stage = static_cast<uint32_t>(resident_load(&sl->stage));
+    if (tid == 0) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // one L1 / L2 invalidation per batch: its records
+    // the slot in one round trip: 16 lanes of wave 0 read a field each
+    if (tid < 16)
+      bc[2 + tid] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&box->slots[seq % kResidentSlots]) + tid,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    const ResidentSlot sl = *reinterpret_cast<const ResidentSlot*>(bc + 2);
+    if (uniform64(sl.kind) != static_cast<uint64_t>(kReg)) return;  // another instantiation: the host relaunches
+    const uint64_t gen = uniform64(sl.gen);
+    const uint32_t* prog = reinterpret_cast<const uint32_t*>(uniform64(sl.prog));
+    const uint8_t* arena = reinterpret_cast<const uint8_t*>(uniform64(sl.arena));
+    const uint64_t* offs = reinterpret_cast<const uint64_t*>(uniform64(sl.offs));
+    int32_t* verdicts = reinterpret_cast<int32_t*>(uniform64(sl.verdicts));
+    const uint64_t arena_bytes = uniform64(sl.arena_bytes), n = uniform64(sl.n);
+    const uint32_t stage = static_cast<uint32_t>(uniform64(sl.stage));
+    ResidentSlot* slp = &box->slots[seq % kResidentSlots];
+    const uint64_t t_read = __builtin_amdgcn_s_memrealtime();
     http_eval_body<kNoHits, kReg, 0, false>(prog, arena, arena_bytes, offs, n, verdicts, nullptr, stage, nullptr,
                                             nullptr, prog != cur || gen != cur_gen, 0, 1);
     cur = prog;
     cur_gen = gen;
-    __threadfence_system();  // this thread's verdict stores before done_seq
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's verdict stores have reached the L2
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(&box->done_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) {
+      const uint64_t t_body = __builtin_amdgcn_s_memrealtime();
+      __threadfence_system();  // one L2 write-back per batch: the verdicts, then done_seq
+      const uint64_t t_sync = __builtin_amdgcn_s_memrealtime();
+      const uint64_t st[4] = {bc[1], t_read, t_body, t_sync};
+      for (int k = 0; k < 4; ++k)
+        __hip_atomic_store(&slp->stamp[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->done_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     ++seq;
   }
 }

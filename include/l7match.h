@@ -394,6 +394,11 @@ int l7m_batcher_stats(l7m_batcher* b, uint64_t* batches, uint64_t* requests);
 typedef struct {
   uint64_t batches, requests;
   double fill_us, launch_us, gpu_us, wake_us;
+  /* batches served by the resident workgroup, and its mean time per batch
+   * reading the slot (incl. cache invalidation), evaluating, and writing the
+   * verdicts back (device clock) */
+  uint64_t resident_batches;
+  double resident_read_us, resident_eval_us, resident_sync_us;
 } l7m_batcher_profile;
 int l7m_batcher_get_profile(l7m_batcher* b, l7m_batcher_profile* out);
 void l7m_batcher_destroy(l7m_batcher* b);

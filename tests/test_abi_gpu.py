@@ -145,10 +145,10 @@ def test_batcher_resident_evaluator_relaunch_and_rule_switch(gpu):
         reqs_b.append(L.HTTPRequest(str(rng.choice(["GET", "POST"])), str(rng.choice(["/a/x", "/b/yz", "/b/9", "/c"])),
                                     str(rng.choice(["h1.example", "h22.example", "hx.example"])), hdr))
     ab, ob = L.pack_http(reqs_b)
-    recs_b = [ab[int(ob[i]):int(ob[i + 1]) if i + 1 < len(ob) else ab.nbytes - 64].tobytes() for i in range(len(ob))]
+    recs_b = [ab[int(ob[i]):int(ob[i + 1]) if i + 1 < len(ob) else ab.nbytes].tobytes() for i in range(len(ob))]
     exp_b = HttpOracle(rules_b).eval(ab, ob)
     ac, oc = L.pack_http(realistic_requests(rng, 300))
-    recs_c = [ac[int(oc[i]):int(oc[i + 1]) if i + 1 < len(oc) else ac.nbytes - 64].tobytes() for i in range(len(oc))]
+    recs_c = [ac[int(oc[i]):int(oc[i + 1]) if i + 1 < len(oc) else ac.nbytes].tobytes() for i in range(len(oc))]
     exp_c = HttpOracle(REALISTIC).eval(ac, oc)
 
     rs_a, rs_b, rs_c = (L.RuleSet.compile_http(r) for r in (rules_a, rules_b, REALISTIC))
