@@ -215,7 +215,7 @@ struct l7m_batcher {
   }
   // (res.mu held) the running instance has ended: its cached programs may go
   void resident_reap_locked() {
-    if (res.running && hipEventQuery(res.end) == hipSuccess) {
+    if (res.running && __atomic_load_n(&res.box->exited, __ATOMIC_ACQUIRE)) {  // it reads no program any more
       res.running = false;
       for (l7m_ruleset* r : res.held) l7m_release(r);
       res.held.clear();
@@ -227,6 +227,7 @@ struct l7m_batcher {
     if (first > res.posted) return true;
     const int kind = static_cast<int>(
         __atomic_load_n(&res.box->slots[first % l7m::kResidentSlots].kind, __ATOMIC_ACQUIRE));
+    __atomic_store_n(&res.box->exited, 0ull, __ATOMIC_RELEASE);
     if (l7m::launch_resident(res.dbox, first, kind, res.qhdr, res.stream) != hipSuccess ||
         hipEventRecord(res.end, res.stream) != hipSuccess)
       return false;
@@ -259,6 +260,7 @@ struct l7m_batcher {
       put(&sl.stage, stage);
       put(&sl.ids, reinterpret_cast<uint64_t>(b->d_ids));
       put(&sl.result, 0);
+      for (uint64_t& x : sl.stamp) put(&x, 0);
       res.slot_rs[seq % l7m::kResidentSlots] = r;
       resident_hold_locked(r);
       __atomic_store_n(&res.box->post_seq, seq, __ATOMIC_RELEASE);
@@ -271,7 +273,7 @@ struct l7m_batcher {
       const l7m::ResidentSlot& sl = res.box->slots[seq % l7m::kResidentSlots];
       uint64_t st[4];
       for (int k = 0; k < 4; ++k) st[k] = __atomic_load_n(&sl.stamp[k], __ATOMIC_ACQUIRE);
-      if (st[3] >= st[2] && st[2] >= st[1] && st[1] >= st[0]) {
+      if (st[0] && st[3] >= st[2] && st[2] >= st[1] && st[1] >= st[0]) {
         res_batches.fetch_add(1);
         res_read.fetch_add(st[1] - st[0]);
         res_eval.fetch_add(st[2] - st[1]);
@@ -281,7 +283,7 @@ struct l7m_batcher {
     };
     for (uint32_t spin = 0;; ++spin) {
       if (__atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= seq) return outcome();
-      if ((spin & 63) == 63) {  // the instance may have exited (idle, or another instantiation)
+      if ((spin & 63) == 63 && __atomic_load_n(&res.box->exited, __ATOMIC_ACQUIRE)) {  // idle exit / other kind
         std::lock_guard<std::mutex> g(res.mu);
         if (__atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= seq) return outcome();
         resident_reap_locked();

@@ -47,7 +47,8 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
 // evaluates the slot and raises done_seq to seq.  Every field is read and
 // written with system-scope atomics.
 constexpr uint32_t kResidentSlots = 16;
-constexpr uint32_t kResidentLdsWords = 40;  // broadcast words (decision + slot copy) at the end of the resident LDS
+constexpr uint32_t kResidentRound = 16;      // slots one resident round evaluates together (one per wave at most)
+constexpr uint32_t kResidentLdsWords = 2 * (4 + 16 * kResidentRound);  // broadcast words at the end of its LDS
 constexpr uint64_t kResidentIdleTicks = 2000000;  // 20 ms of s_memrealtime (100 MHz) without work: exit
 constexpr uint64_t kResidentKafka = 16;          // kind of a Kafka slot: kResidentKafka | cli_lds | groups << 1
 struct ResidentSlot {
@@ -65,6 +66,7 @@ struct ResidentBox {
   alignas(64) uint64_t post_seq;
   alignas(64) uint64_t done_seq;
   alignas(64) uint64_t quit;
+  alignas(64) uint64_t exited;  // set by the workgroup as it returns (cleared by the host before a launch)
   alignas(64) ResidentSlot slots[kResidentSlots];
 };
 // Whether a program can be served by the resident evaluator (no search

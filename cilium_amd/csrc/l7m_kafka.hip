@@ -832,6 +832,9 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {  // uniform: in SGPR
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
+__device__ __forceinline__ void resident_exit(ResidentBox* box) {
+  if (threadIdx.x == 0) __hip_atomic_store(&box->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
   return uniform64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
@@ -867,7 +870,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_resident_kernel(ResidentBox* bo
     __syncthreads();
     const uint64_t act = bc[0];
     __syncthreads();
-    if (!act) return;
+    if (!act) return resident_exit(box);
     if (tid == 0) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // one L1 / L2 invalidation per batch
     ResidentSlot* slp = &box->slots[seq % kResidentSlots];
     if (tid < 16)  // the slot in one round trip
@@ -875,7 +878,7 @@ __global__ __launch_bounds__(kKBlock) void kafka_resident_kernel(ResidentBox* bo
                                       __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
     const ResidentSlot sl = *reinterpret_cast<const ResidentSlot*>(bc + 2);
-    if (uniform64(sl.kind) != my_kind) return;  // another instantiation: the host relaunches
+    if (uniform64(sl.kind) != my_kind) return resident_exit(box);  // another instantiation: the host relaunches
     const uint64_t gen = uniform64(sl.gen);
     const uint32_t* prog = reinterpret_cast<const uint32_t*>(uniform64(sl.prog));
     const uint8_t* arena = reinterpret_cast<const uint8_t*>(uniform64(sl.arena));
