@@ -219,13 +219,13 @@ int main(int argc, char** argv) {
     printf("{\"threads\": %d, \"eager\": %d, \"verdicts_per_s\": %.1f, \"p50_us\": %.1f, \"p99_us\": %.1f, "
            "\"max_us\": %.1f, \"batches\": %llu, \"mean_batch\": %.1f, \"requests\": %llu, \"mismatches\": %llu, "
            "\"phases_us\": {\"fill\": %.2f, \"launch\": %.2f, \"gpu\": %.2f, \"wake\": %.2f}, "
-           "\"resident\": {\"batches\": %llu, \"read_us\": %.2f, \"eval_us\": %.2f, \"sync_us\": %.2f}, "
+           "\"resident\": {\"batches\": %llu, \"rounds\": %llu, \"read_us\": %.2f, \"eval_us\": %.2f, \"sync_us\": %.2f}, "
            "\"cgroup_nr_throttled\": %lld, \"cgroup_throttled_usec\": %lld}\n",
            T, eager, done / dt, done ? all[done / 2] : 0.0, done ? all[(uint64_t)(done * 0.99)] : 0.0,
            done ? all[done - 1] : 0.0, (unsigned long long)(b1 - b0),
            (b1 - b0) ? (double)(r1 - r0) / (double)(b1 - b0) : 0.0, (unsigned long long)done,
            (unsigned long long)bad, pf.fill_us, pf.launch_us, pf.gpu_us, pf.wake_us,
-           (unsigned long long)pf.resident_batches, pf.resident_read_us, pf.resident_eval_us, pf.resident_sync_us,
+           (unsigned long long)pf.resident_batches, (unsigned long long)pf.resident_rounds, pf.resident_read_us, pf.resident_eval_us, pf.resident_sync_us,
            thr0 >= 0 ? thr1 - thr0 : -1, thu0 >= 0 ? thu1 - thu0 : -1);
     fflush(stdout);
     free(all);

@@ -339,7 +339,7 @@ struct l7m_batcher {
         // idle: poll a little, then sleep until a caller's first append
         const int64_t t0 = now_ns();
         bool work = false;
-        while (now_ns() - t0 < 20000) {
+        while (now_ns() - t0 < 100000) {  // 100 us: a busy proxy's next request usually comes sooner
           if (count_of(cur.load(std::memory_order_acquire)->resv.load(std::memory_order_acquire)) || stop.load()) {
             work = true;
             break;
@@ -601,6 +601,7 @@ int l7m_batcher_get_profile(l7m_batcher* b, l7m_batcher_profile* out) {
   out->gpu_us = nb ? b->gpu_ns.load() / 1e3 / nb : 0.0;
   const uint64_t rb = b->res_batches.load();
   out->resident_batches = rb;
+  out->resident_rounds = b->res.box ? __atomic_load_n(&b->res.box->rounds, __ATOMIC_ACQUIRE) : 0;
   out->resident_read_us = rb ? b->res_read.load() / 100.0 / rb : 0.0;  // 100 ticks per us
   out->resident_eval_us = rb ? b->res_eval.load() / 100.0 / rb : 0.0;
   out->resident_sync_us = rb ? b->res_sync.load() / 100.0 / rb : 0.0;

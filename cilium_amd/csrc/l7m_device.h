@@ -67,6 +67,7 @@ struct ResidentBox {
   alignas(64) uint64_t done_seq;
   alignas(64) uint64_t quit;
   alignas(64) uint64_t exited;  // set by the workgroup as it returns (cleared by the host before a launch)
+  alignas(64) uint64_t rounds;  // rounds evaluated (statistics)
   alignas(64) ResidentSlot slots[kResidentSlots];
 };
 // Whether a program can be served by the resident evaluator (no search

@@ -633,7 +633,7 @@ __device__ __forceinline__ void kafka_eval_body(const uint32_t* __restrict__ pro
                                                 unsigned long long* __restrict__ hits, uint32_t stage,
                                                 uint32_t* __restrict__ crecs, uint32_t* qhdr, uint32_t qcap,
                                                 const uint32_t* __restrict__ ids, bool load_tables, uint32_t part,
-                                                uint32_t nparts) {
+                                                uint32_t nparts, uint32_t wave_index, uint32_t wave_count) {
   extern __shared__ __align__(16) uint32_t ksmem[];
   uint64_t prof[5] = {0, 0, 0, 0, 0};  // (kProf diagnostic builds)
   const KafkaHeader& h = *reinterpret_cast<const KafkaHeader*>(prog);
@@ -674,8 +674,8 @@ __device__ __forceinline__ void kafka_eval_body(const uint32_t* __restrict__ pro
   v.strings = reinterpret_cast<const uint8_t*>(prog + h.off_strings);
   v.n_slots = kAblate == 2 ? 0 : h.n_slots;
 
-  const uint64_t gw = static_cast<uint64_t>(part) * kKWaves + wv;
-  const uint64_t nw = static_cast<uint64_t>(nparts) * kKWaves;
+  const uint64_t gw = wave_index;  // this wave's share of the batch: wave wave_index of wave_count
+  const uint64_t nw = wave_count;
   const uint64_t end = n * (gw + 1) / nw;
   struct Tile {
     uint64_t cur, o, onext, base;
@@ -824,7 +824,8 @@ __global__ __launch_bounds__(kKBlock) void kafka_eval_kernel(const uint32_t* __r
                                                              uint32_t* __restrict__ crecs, uint32_t* qhdr,
                                                              uint32_t qcap, const uint32_t* __restrict__ ids) {
   kafka_eval_body<kHits, kAblate, kCliLds, kGroups>(prog, arena, arena_bytes, offs, n, verdicts, hits, stage, crecs,
-                                                    qhdr, qcap, ids, true, blockIdx.x, gridDim.x);
+                                                    qhdr, qcap, ids, true, blockIdx.x, gridDim.x,
+                                                    blockIdx.x * kKWaves + (threadIdx.x >> 6), gridDim.x * kKWaves);
 }
 
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {  // uniform: in SGPRs
@@ -847,66 +848,80 @@ __device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
 template <bool kCliLds, bool kGroups>
 __global__ __launch_bounds__(kKBlock) void kafka_resident_kernel(ResidentBox* box, uint64_t seq, uint32_t* qhdr) {
   extern __shared__ __align__(16) uint32_t ksmem[];
-  const uint32_t tid = threadIdx.x;
-  uint64_t* bc = reinterpret_cast<uint64_t*>(ksmem + kKLdsBytes / 4 - kResidentLdsWords);
+  const uint32_t tid = threadIdx.x, wv = tid >> 6;
+  uint64_t* bc = reinterpret_cast<uint64_t*>(ksmem + kKLdsBytes / 4 - kResidentLdsWords);  // as http_resident_kernel
   const uint32_t* cur = nullptr;
-  uint64_t cur_gen = 0;
+  uint64_t cur_gen = 0, rounds = resident_load(&box->rounds);
   const uint64_t my_kind = kResidentKafka | (kCliLds ? 1u : 0u) | (kGroups ? 2u : 0u);
   for (;;) {
     if (tid == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      uint64_t act = 0;
-      for (;;) {
-        if (resident_load(&box->post_seq) >= seq) {
+      uint64_t act = 0, ps = 0;
+      for (uint32_t it = 1;; ++it) {  // one host-memory read per poll; quit and the idle limit every 64th
+        ps = resident_load(&box->post_seq);
+        if (ps >= seq) {
           act = 1;
           break;
         }
-        if (resident_load(&box->quit) || __builtin_amdgcn_s_memrealtime() - t0 > kResidentIdleTicks) break;
-        __builtin_amdgcn_s_sleep(1);
+        if (!(it & 63) && (resident_load(&box->quit) || __builtin_amdgcn_s_memrealtime() - t0 > kResidentIdleTicks))
+          break;
       }
       bc[0] = act;
       bc[1] = __builtin_amdgcn_s_memrealtime();
+      bc[2] = ps;
+      if (act) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // one L1 / L2 invalidation per round: its records
     }
     __syncthreads();
     const uint64_t act = bc[0];
+    const uint32_t pend = static_cast<uint32_t>(
+        act ? (bc[2] - seq + 1 < kResidentRound ? bc[2] - seq + 1 : kResidentRound) : 0);
+    if (tid < 16 * pend)  // every posted slot in one round trip
+      bc[4 + tid] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&box->slots[(seq + tid / 16) % kResidentSlots]) +
+                                          (tid & 15u),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
     if (!act) return resident_exit(box);
-    if (tid == 0) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // one L1 / L2 invalidation per batch
-    ResidentSlot* slp = &box->slots[seq % kResidentSlots];
-    if (tid < 16)  // the slot in one round trip
-      bc[2 + tid] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(slp) + tid, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
-    const ResidentSlot sl = *reinterpret_cast<const ResidentSlot*>(bc + 2);
-    if (uniform64(sl.kind) != my_kind) return resident_exit(box);  // another instantiation: the host relaunches
-    const uint64_t gen = uniform64(sl.gen);
-    const uint32_t* prog = reinterpret_cast<const uint32_t*>(uniform64(sl.prog));
+    const ResidentSlot* rs = reinterpret_cast<const ResidentSlot*>(bc + 4);
+    if (uniform64(rs[0].kind) != my_kind) return resident_exit(box);  // another instantiation: the host relaunches
+    const uint64_t gen = uniform64(rs[0].gen), prog0 = uniform64(rs[0].prog);
+    uint32_t nb = 1;
+    while (nb < pend && rs[nb].kind == rs[0].kind && rs[nb].gen == gen && rs[nb].prog == prog0) ++nb;
+    nb = __builtin_amdgcn_readfirstlane(nb);
+    const uint32_t b = wv % nb, wi = wv / nb, wc = (kKWaves - b + nb - 1) / nb;
+    const ResidentSlot& sl = rs[b];
+    const uint32_t* prog = reinterpret_cast<const uint32_t*>(prog0);
     const uint8_t* arena = reinterpret_cast<const uint8_t*>(uniform64(sl.arena));
     const uint64_t* offs = reinterpret_cast<const uint64_t*>(uniform64(sl.offs));
     int32_t* verdicts = reinterpret_cast<int32_t*>(uniform64(sl.verdicts));
     const uint32_t* ids = reinterpret_cast<const uint32_t*>(uniform64(sl.ids));
     const uint64_t arena_bytes = uniform64(sl.arena_bytes), n = uniform64(sl.n);
-    const uint32_t stage = static_cast<uint32_t>(uniform64(sl.stage));
+    const uint32_t stage = static_cast<uint32_t>(uniform64(rs[0].stage));
     const uint64_t t_read = __builtin_amdgcn_s_memrealtime();
     kafka_eval_body<kKNoHits, 0, kCliLds, kGroups>(prog, arena, arena_bytes, offs, n, verdicts, nullptr, stage,
-                                                   nullptr, qhdr, 0, ids, prog != cur || gen != cur_gen, 0, 1);
+                                                   nullptr, qhdr, 0, ids, prog != cur || gen != cur_gen, 0, 1, wi, wc);
     cur = prog;
     cur_gen = gen;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
       const uint64_t t_body = __builtin_amdgcn_s_memrealtime();
-      __threadfence_system();  // one L2 write-back per batch: the verdicts, then done_seq
+      __threadfence_system();  // one L2 write-back per round: the verdicts, then done_seq
       const uint64_t t_sync = __builtin_amdgcn_s_memrealtime();
       const uint64_t st[4] = {bc[1], t_read, t_body, t_sync};
-      for (int k = 0; k < 4; ++k)
-        __hip_atomic_store(&slp->stamp[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // a compressed set anywhere in the round: its batches go to the normal launches
       const uint32_t queued = __hip_atomic_load(qhdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(qhdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&slp->result, queued ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&box->done_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (uint32_t q = 0; q < nb; ++q) {
+        ResidentSlot* slp = &box->slots[(seq + q) % kResidentSlots];
+        for (int k = 0; k < 4; ++k)
+          __hip_atomic_store(&slp->stamp[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&slp->result, queued ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __hip_atomic_store(&box->rounds, ++rounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->done_seq, seq + nb - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    ++seq;
+    seq += nb;
+    __syncthreads();  // bc is rewritten by the next round
   }
 }
 

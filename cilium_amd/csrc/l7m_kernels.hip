@@ -1347,19 +1347,19 @@ __global__ __launch_bounds__(kBlock) void http_resident_kernel(ResidentBox* box,
   // [4 + 16 b ...] slot b of this round
   uint64_t* bc = reinterpret_cast<uint64_t*>(smem + kHttpLdsBytes / 4 - kResidentLdsWords);
   const uint32_t* cur = nullptr;
-  uint64_t cur_gen = 0;
+  uint64_t cur_gen = 0, rounds = resident_load(&box->rounds);
   for (;;) {
     if (tid == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       uint64_t act = 0, ps = 0;
-      for (;;) {
+      for (uint32_t it = 1;; ++it) {  // one host-memory read per poll; quit and the idle limit every 64th
         ps = resident_load(&box->post_seq);
         if (ps >= seq) {
           act = 1;
           break;
         }
-        if (resident_load(&box->quit) || __builtin_amdgcn_s_memrealtime() - t0 > kResidentIdleTicks) break;
-        __builtin_amdgcn_s_sleep(1);
+        if (!(it & 63) && (resident_load(&box->quit) || __builtin_amdgcn_s_memrealtime() - t0 > kResidentIdleTicks))
+          break;
       }
       bc[0] = act;
       bc[1] = __builtin_amdgcn_s_memrealtime();
@@ -1408,6 +1408,7 @@ __global__ __launch_bounds__(kBlock) void http_resident_kernel(ResidentBox* box,
         for (int k = 0; k < 4; ++k)
           __hip_atomic_store(&slp->stamp[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
+      __hip_atomic_store(&box->rounds, ++rounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&box->done_seq, seq + nb - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     seq += nb;

@@ -145,7 +145,8 @@ class _NetworkPolicy(ctypes.Structure):
 class _BatcherProfile(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("fill_us", ctypes.c_double),
                 ("launch_us", ctypes.c_double), ("gpu_us", ctypes.c_double), ("wake_us", ctypes.c_double),
-                ("resident_batches", ctypes.c_uint64), ("resident_read_us", ctypes.c_double),
+                ("resident_batches", ctypes.c_uint64), ("resident_rounds", ctypes.c_uint64),
+                ("resident_read_us", ctypes.c_double),
                 ("resident_eval_us", ctypes.c_double), ("resident_sync_us", ctypes.c_double)]
 
 
@@ -690,7 +691,7 @@ class Batcher:
         p = _BatcherProfile()
         _lib.l7m_batcher_get_profile(self._h, ctypes.byref(p))
         return {"batches": p.batches, "requests": p.requests, "fill_us": p.fill_us, "launch_us": p.launch_us,
-                "gpu_us": p.gpu_us, "wake_us": p.wake_us, "resident_batches": p.resident_batches,
+                "gpu_us": p.gpu_us, "wake_us": p.wake_us, "resident_batches": p.resident_batches, "resident_rounds": p.resident_rounds,
                 "resident_read_us": p.resident_read_us, "resident_eval_us": p.resident_eval_us,
                 "resident_sync_us": p.resident_sync_us}
 

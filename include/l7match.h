@@ -397,7 +397,7 @@ typedef struct {
   /* batches served by the resident workgroup, and its mean time per batch
    * reading the slot (incl. cache invalidation), evaluating, and writing the
    * verdicts back (device clock) */
-  uint64_t resident_batches;
+  uint64_t resident_batches, resident_rounds; /* rounds: one or more batches evaluated together */
   double resident_read_us, resident_eval_us, resident_sync_us;
 } l7m_batcher_profile;
 int l7m_batcher_get_profile(l7m_batcher* b, l7m_batcher_profile* out);
