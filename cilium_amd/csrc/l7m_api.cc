@@ -394,25 +394,19 @@ int eval_pipelined(EvalCtx* c, const l7m_ruleset* rs, const uint8_t* arena, size
 namespace l7m {
 
 // The batcher's resident evaluator (l7m_batch.cc): whether the rule set can
-// be served by http_resident_kernel, with its device program, instantiation,
+// be served by kafka_resident_kernel, with its device program, instantiation,
 // record stage and serial.
 bool resident_program(l7m_ruleset* rs, const uint32_t** dprog, int* kind, uint32_t* stage, uint64_t* serial) {
-  if (rs->proto != L7M_PROTO_HTTP && rs->proto != L7M_PROTO_KAFKA) return false;
+  // Kafka only: for HTTP the launch per batch measured faster (config 2, 8
+  // callers: 165 k/s at p50 47 us launched vs 158 k/s at p50 51 us resident,
+  // profiles/r04/ab_round4.md)
+  if (rs->proto != L7M_PROTO_KAFKA) return false;
   int cus = 0;
   if (device_program(rs, dprog, &cus) != L7M_OK) return false;
   *serial = rs->serial;
-  if (rs->proto == L7M_PROTO_KAFKA) {
-    KafkaHeader kh;
-    std::memcpy(&kh, rs->program.data(), sizeof kh);
-    return kafka_resident_ok(kh, kind, stage);
-  }
-  HttpHeader h;
-  std::memcpy(&h, rs->program.data(), sizeof h);
-  uint32_t flags = 0;
-  const DfaDesc* dd = reinterpret_cast<const DfaDesc*>(rs->program.data() + h.off_dfas);
-  for (uint32_t k = 0; k < h.n_dfas; ++k)
-    if (dd[k].lit_tab != kNone) flags |= kLaunchLiterals;
-  return http_resident_ok(h, flags, kind, stage);
+  KafkaHeader kh;
+  std::memcpy(&kh, rs->program.data(), sizeof kh);
+  return kafka_resident_ok(kh, kind, stage);
 }
 
 }  // namespace l7m

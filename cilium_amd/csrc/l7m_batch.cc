@@ -160,9 +160,12 @@ struct l7m_batcher {
   std::atomic<uint64_t> batches{0}, requests{0}, fill_ns{0}, launch_ns{0}, gpu_ns{0}, wake_ns{0};
   std::atomic<uint64_t> res_batches{0}, res_read{0}, res_eval{0}, res_sync{0};  // device ticks (100 MHz)
 
-  // Resident evaluator (l7m_kernels.hip http_resident_kernel): batches of
-  // up to kResidentMax HTTP records whose program it can serve are posted to
-  // a workgroup that stays on the GPU, instead of launching a kernel each.
+  // Resident evaluator (l7m_kafka.hip kafka_resident_kernel): Kafka batches
+  // of up to kResidentMax records are posted to a workgroup that stays on the
+  // GPU instead of launching the first pass and the codec pass each (config
+  // 3, 8 callers: 105 k/s at p50 72 us launched -> 163-177 k/s at p50 45-49
+  // us).  HTTP batches are launched: the resident HTTP workgroup measured
+  // slower than a launch (profiles/r04/ab_round4.md).
   static constexpr uint32_t kResidentMax = 1024;
   struct Resident {
     std::mutex mu;

@@ -41,7 +41,7 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags);
 
-// Mailbox of a resident HTTP evaluator (l7m_kernels.hip http_resident_kernel),
+// Mailbox of a resident evaluator (l7m_kafka.hip kafka_resident_kernel),
 // in pinned, device-mapped host memory.  The host fills slot seq %
 // kResidentSlots, then raises post_seq to seq (release); the workgroup
 // evaluates the slot and raises done_seq to seq.  Every field is read and
@@ -52,7 +52,7 @@ constexpr uint32_t kResidentLdsWords = 2 * (4 + 16 * kResidentRound);  // broadc
 constexpr uint64_t kResidentIdleTicks = 2000000;  // 20 ms of s_memrealtime (100 MHz) without work: exit
 constexpr uint64_t kResidentKafka = 16;          // kind of a Kafka slot: kResidentKafka | cli_lds | groups << 1
 struct ResidentSlot {
-  uint64_t kind;  // the instantiation: HTTP kReg (4 or 8), or kResidentKafka | ...
+  uint64_t kind;  // the instantiation: kResidentKafka | cli_lds | groups << 1
   uint64_t gen;   // program generation (a new program at a reused address reloads the image)
   uint64_t prog, arena, arena_bytes, offs, n, verdicts, stage, ids;
   uint64_t result;  // written by the workgroup: 1 = evaluate this batch again with the normal launches
@@ -70,15 +70,12 @@ struct ResidentBox {
   alignas(64) uint64_t rounds;  // rounds evaluated (statistics)
   alignas(64) ResidentSlot slots[kResidentSlots];
 };
-// Whether a program can be served by the resident evaluator (no search
-// automata, slow-path rules or literal tables, <= 8 value DFAs) and with
+// Whether a Kafka program can be served by the resident evaluator, with
 // which instantiation and record stage.
-bool http_resident_ok(const HttpHeader& h, uint32_t flags, int* kind, uint32_t* stage);
 bool kafka_resident_ok(const KafkaHeader& h, int* kind, uint32_t* stage);
 // Launch the resident workgroup of `kind` for slots first_seq, ...; qhdr: 16
 // bytes of zeroed device memory (the Kafka instantiations' queue counter).
 hipError_t launch_resident(ResidentBox* dbox, uint64_t first_seq, int kind, uint32_t* qhdr, hipStream_t stream);
-hipError_t launch_http_resident(ResidentBox* dbox, uint64_t first_seq, int kind, hipStream_t stream);
 hipError_t launch_kafka_resident(ResidentBox* dbox, uint64_t first_seq, int kind, uint32_t* qhdr,
                                  hipStream_t stream);
 

@@ -840,8 +840,20 @@ __device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
   return uniform64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 
-// Resident Kafka evaluator: the mailbox protocol of http_resident_kernel
-// (l7m_kernels.hip), one workgroup.  Requests with compressed message sets
+// Resident Kafka evaluator for the batcher's small batches (l7m_batch.cc):
+// ONE workgroup stays on the GPU and polls a mailbox in pinned host memory
+// (ResidentBox, l7m_device.h), so a batch costs no kernel launch, no
+// completion signal and no LDS table load (kept while the program is the
+// same).  Per round: wait until post_seq reaches the next sequence number,
+// read every posted slot (one per wave group), evaluate them together with
+// the kafka_eval_kernel code, publish done_seq.  Exit (every wave takes the
+// same branch after a barrier): quit set by the host, a slot for another
+// instantiation (the host relaunches the right one), or kResidentIdleTicks
+// of s_memrealtime without work, so the workgroup drains by itself when its
+// process ends.  Memory: mailbox fields are read and written with relaxed
+// system-scope atomics; per round one thread invalidates the L1 / L2 before
+// the records are read and one writes the L2 back after every thread's
+// verdict stores have been acknowledged.  Requests with compressed message sets
 // need the codec pass (kafka_codec_kernel): the resident workgroup has no
 // queue (capacity 0), counts them, and reports the batch back (slot.result
 // = 1) so the host evaluates that batch with the normal launches.
@@ -849,7 +861,8 @@ template <bool kCliLds, bool kGroups>
 __global__ __launch_bounds__(kKBlock) void kafka_resident_kernel(ResidentBox* box, uint64_t seq, uint32_t* qhdr) {
   extern __shared__ __align__(16) uint32_t ksmem[];
   const uint32_t tid = threadIdx.x, wv = tid >> 6;
-  uint64_t* bc = reinterpret_cast<uint64_t*>(ksmem + kKLdsBytes / 4 - kResidentLdsWords);  // as http_resident_kernel
+  // broadcast: [0] decision, [1] detection time, [2] post_seq seen, [4 + 16 b ...] slot b
+  uint64_t* bc = reinterpret_cast<uint64_t*>(ksmem + kKLdsBytes / 4 - kResidentLdsWords);
   const uint32_t* cur = nullptr;
   uint64_t cur_gen = 0, rounds = resident_load(&box->rounds);
   const uint64_t my_kind = kResidentKafka | (kCliLds ? 1u : 0u) | (kGroups ? 2u : 0u);

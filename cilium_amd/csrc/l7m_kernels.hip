@@ -87,27 +87,6 @@ struct GlbSrc {
   }
 };
 
-// Records in pinned host memory read by the resident evaluator: system-scope
-// loads (sc0 sc1: around the L2, so no invalidation is needed between
-// batches).
-struct SysSrc {
-  static constexpr bool kLds = false;
-  const uint32_t* w;
-  __device__ __forceinline__ uint32_t word(uint32_t i) const {
-    return __hip_atomic_load(w + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __device__ __forceinline__ uint32_t byte(uint32_t i) const { return (word(i >> 2) >> (8 * (i & 3u))) & 0xffu; }
-  __device__ __forceinline__ uint32_t word_u(uint32_t p) const {
-    return __builtin_amdgcn_alignbyte(word((p >> 2) + 1), word(p >> 2), p & 3u);
-  }
-};
-constexpr int kCpolSys = 19;  // sc0 | nt | sc1: a system-coherent LDS-DMA load
-template <bool kSys>
-__device__ __forceinline__ uint64_t sys_ld64(const uint64_t* p) {
-  if constexpr (kSys) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return *p;
-}
-
 // End code of a finished walk (final base, slot of the last transition taken
 // from a multi-pattern state).
 template <bool kLdsTab>
@@ -1068,11 +1047,10 @@ enum HitMode { kNoHits = 0, kLdsHits = 1, kGlobalHits = 2 };
 #else
 #define L7M_HTTP_OCC
 #endif
-// The evaluation of one batch by one workgroup, `part` of `nparts` (the
-// grid of http_eval_kernel, or the single workgroup of http_resident_kernel,
-// which keeps the LDS image of the previous batch when the program is the
-// same: load_image false).
-template <int kHits, int kReg, int kAblate, bool kLit, bool kSys = false>
+// The evaluation of one batch by one workgroup, `part` of `nparts` of the
+// grid; each wave takes share wave_index of wave_count (load_image false
+// would keep an LDS image already in place).
+template <int kHits, int kReg, int kAblate, bool kLit>
 __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog, const uint8_t* __restrict__ arena,
                                                uint64_t arena_bytes, const uint64_t* __restrict__ offs, uint64_t n,
                                                int32_t* __restrict__ verdicts, unsigned long long* __restrict__ hits,
@@ -1137,8 +1115,8 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
     *o = 0;
     *onext = 0;
     if (cur < end && lane < end - cur) {
-      *o = sys_ld64<kSys>(offs + cur + lane);
-      *onext = cur + lane + 1 < n ? sys_ld64<kSys>(offs + cur + lane + 1) : arena_bytes;
+      *o = offs[cur + lane];
+      *onext = cur + lane + 1 < n ? offs[cur + lane + 1] : arena_bytes;
     }
   };
   auto plan = [&](uint64_t cur, uint64_t o, uint64_t onext) -> Tile {
@@ -1182,7 +1160,7 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
                                          reinterpret_cast<__attribute__((address_space(3))) void*>(
                                              reinterpret_cast<uintptr_t>(stg + it * 1024u)),
-                                         16, 0, kSys ? kCpolSys : 2);
+                                         16, 0, 2);
     }
   };
   uint64_t o1, n1, o2, n2;
@@ -1217,13 +1195,8 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
       }
       if (!done) {  // outside the staged window: read HBM directly
         const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
-        if constexpr (kSys) {
-          const SysSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-          v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo, prof) : L7M_VERDICT_PARSE_ERROR;
-        } else {
-          const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-          v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo, prof) : L7M_VERDICT_PARSE_ERROR;
-        }
+        const GlbSrc s{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
+        v = inb ? eval_walk<kReg, kAblate, kLit>(c, h, s, arena_bytes - o, wo, prof) : L7M_VERDICT_PARSE_ERROR;
       }
     }
     qtn(1);
@@ -1237,8 +1210,7 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
     qtn(3);
     if (lane < take) {
       if (v == kNeedVerify) v = eval_verify<kReg>(c, h, wo);
-      if constexpr (kSys) __hip_atomic_store(verdicts + t.cur + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      else verdicts[t.cur + lane] = v;
+      verdicts[t.cur + lane] = v;
       if (v == kDeferred) {  // decided by http_slow_kernel (rules with slow-path matchers)
         const uint32_t at = atomicAdd(slowq, 1u);
         slowq[1 + at] = static_cast<uint32_t>(t.cur + lane);
@@ -1303,117 +1275,6 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
   http_eval_body<kHits, kReg, kAblate, kLit>(prog, arena, arena_bytes, offs, n, verdicts, hits, stage, scratch, slowq,
                                              true, blockIdx.x, gridDim.x, blockIdx.x * kWaves + (threadIdx.x >> 6),
                                              gridDim.x * kWaves);
-}
-
-// Resident evaluator for small batches (the batcher's per-request latency
-// path, l7m_batch.cc): ONE workgroup stays on the GPU and polls a mailbox in
-// pinned host memory (ResidentBox, l7m_device.h) for posted batches, so a
-// batch costs no kernel launch, no completion signal and no LDS image load
-// (the image is kept while the program is the same).  Per batch: wait until
-// post_seq reaches the next sequence number, read its slot, evaluate it with
-// the http_eval_kernel code (records and verdicts in pinned host memory),
-// publish done_seq.  Exit (every wave takes the same branch after a barrier):
-// quit set by the host, a slot for another instantiation (the host relaunches
-// the right one), or kResidentIdleTicks of s_memrealtime (100 MHz) without
-// work, so the workgroup drains by itself when its process ends.
-// Memory model: every access to host memory — mailbox, offsets, records
-// (LDS-DMA with sc0 sc1), verdicts — is system-coherent (sc0 sc1: it goes
-// around the L1 / L2), so no cache is invalidated or written back between
-// batches and the program's tables stay cached; a batch is published by
-// s_waitcnt vmcnt(0) in every thread (its verdict stores acknowledged), a
-// barrier and one system-scope store of done_seq (PCIe keeps posted writes in
-// order).  (Acquire / release fences per thread cost ~200 us per batch,
-// gpurun_out/r04f; one invalidation + write-back per batch ~11 us of
-// evaluation, r04h.)
-// (a uniform value: moved to SGPRs, so the program header is read with
-// scalar loads as in http_eval_kernel; the host keeps every program it posts
-// alive until the instance ends, so no cached line goes stale)
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
-  return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-__device__ __forceinline__ void resident_exit(ResidentBox* box) {
-  if (threadIdx.x == 0) __hip_atomic_store(&box->exited, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t resident_load(const uint64_t* p) {
-  return uniform64(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-}
-template <int kReg>
-__global__ __launch_bounds__(kBlock) void http_resident_kernel(ResidentBox* box, uint64_t seq) {
-  extern __shared__ __align__(16) uint32_t smem[];
-  const uint32_t tid = threadIdx.x, wv = tid >> 6;
-  // broadcast area: [0] decision, [1] detection time, [2] post_seq seen,
-  // [4 + 16 b ...] slot b of this round
-  uint64_t* bc = reinterpret_cast<uint64_t*>(smem + kHttpLdsBytes / 4 - kResidentLdsWords);
-  const uint32_t* cur = nullptr;
-  uint64_t cur_gen = 0, rounds = resident_load(&box->rounds);
-  for (;;) {
-    if (tid == 0) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      uint64_t act = 0, ps = 0;
-      for (uint32_t it = 1;; ++it) {  // one host-memory read per poll; quit and the idle limit every 64th
-        ps = resident_load(&box->post_seq);
-        if (ps >= seq) {
-          act = 1;
-          break;
-        }
-        if (!(it & 63) && (resident_load(&box->quit) || __builtin_amdgcn_s_memrealtime() - t0 > kResidentIdleTicks))
-          break;
-      }
-      bc[0] = act;
-      bc[1] = __builtin_amdgcn_s_memrealtime();
-      bc[2] = ps;
-    }
-    __syncthreads();
-    const uint64_t act = bc[0];
-    // every posted slot (up to one per wave) in one round trip: thread t
-    // reads word t % 16 of slot t / 16
-    const uint32_t pend = static_cast<uint32_t>(
-        act ? (bc[2] - seq + 1 < kResidentRound ? bc[2] - seq + 1 : kResidentRound) : 0);
-    if (tid < 16 * pend)
-      bc[4 + tid] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(&box->slots[(seq + tid / 16) % kResidentSlots]) +
-                                          (tid & 15u),
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __syncthreads();
-    if (!act) return resident_exit(box);
-    const ResidentSlot* rs = reinterpret_cast<const ResidentSlot*>(bc + 4);
-    if (uniform64(rs[0].kind) != static_cast<uint64_t>(kReg)) return resident_exit(box);  // the host relaunches
-    // this round: the leading slots of the same program
-    const uint64_t gen = uniform64(rs[0].gen), prog0 = uniform64(rs[0].prog);
-    uint32_t nb = 1;
-    while (nb < pend && rs[nb].kind == rs[0].kind && rs[nb].gen == gen && rs[nb].prog == prog0) ++nb;
-    nb = __builtin_amdgcn_readfirstlane(nb);
-    // wave w evaluates batch w % nb, as wave w / nb of the waves given to it
-    const uint32_t b = wv % nb, wi = wv / nb, wc = (kWaves - b + nb - 1) / nb;
-    const ResidentSlot& sl = rs[b];
-    const uint32_t* prog = reinterpret_cast<const uint32_t*>(prog0);
-    const uint8_t* arena = reinterpret_cast<const uint8_t*>(uniform64(sl.arena));
-    const uint64_t* offs = reinterpret_cast<const uint64_t*>(uniform64(sl.offs));
-    int32_t* verdicts = reinterpret_cast<int32_t*>(uniform64(sl.verdicts));
-    const uint64_t arena_bytes = uniform64(sl.arena_bytes), n = uniform64(sl.n);
-    const uint32_t stage = static_cast<uint32_t>(uniform64(rs[0].stage));
-    const uint64_t t_read = __builtin_amdgcn_s_memrealtime();
-    http_eval_body<kNoHits, kReg, 0, false, true>(prog, arena, arena_bytes, offs, n, verdicts, nullptr, stage,
-                                                  nullptr, nullptr, prog != cur || gen != cur_gen, 0, 1, wi, wc);
-    cur = prog;
-    cur_gen = gen;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's verdict stores are acknowledged
-    __syncthreads();
-    if (tid == 0) {
-      const uint64_t t_body = __builtin_amdgcn_s_memrealtime();
-      const uint64_t st[4] = {bc[1], t_read, t_body, t_body};
-      for (uint32_t q = 0; q < nb; ++q) {
-        ResidentSlot* slp = &box->slots[(seq + q) % kResidentSlots];
-        for (int k = 0; k < 4; ++k)
-          __hip_atomic_store(&slp->stamp[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      __hip_atomic_store(&box->rounds, ++rounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&box->done_seq, seq + nb - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    seq += nb;
-    __syncthreads();  // bc is rewritten by the next round
-  }
 }
 
 // Second pass over the requests the first pass deferred (a slow-path rule may
@@ -1516,35 +1377,8 @@ static hipError_t launch_slow(const HttpHeader& h, hipStream_t stream, const uin
   return hipGetLastError();
 }
 
-bool http_resident_ok(const HttpHeader& h, uint32_t flags, int* kind, uint32_t* stage) {
-  if (h.search || h.n_slow || (flags & kLaunchLiterals) || h.n_dfas > kRegDfas) return false;
-  const uint32_t s = http_stage_bytes(h);
-  if (s == 0) return false;
-  // the resident workgroup keeps kResidentLdsWords at the end of the LDS
-  uint32_t st = s;
-  while (st > 256 && http_lds_bytes(h, st) + 4u * kResidentLdsWords > kHttpLdsBytes) st -= 16;
-  if (http_lds_bytes(h, st) + 4u * kResidentLdsWords > kHttpLdsBytes) return false;
-  *kind = h.n_dfas <= 4 ? 4 : 8;
-  *stage = st;
-  return true;
-}
-
 hipError_t launch_resident(ResidentBox* dbox, uint64_t first_seq, int kind, uint32_t* qhdr, hipStream_t stream) {
-  if (static_cast<uint64_t>(kind) & kResidentKafka) return launch_kafka_resident(dbox, first_seq, kind, qhdr, stream);
-  return launch_http_resident(dbox, first_seq, kind, stream);
-}
-
-hipError_t launch_http_resident(ResidentBox* dbox, uint64_t first_seq, int kind, hipStream_t stream) {
-  if (kind == 4) {
-    const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_resident_kernel<4>), kHttpLdsBytes);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(http_resident_kernel<4>, dim3(1), dim3(kBlock), kHttpLdsBytes, stream, dbox, first_seq);
-  } else {
-    const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_resident_kernel<8>), kHttpLdsBytes);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(http_resident_kernel<8>, dim3(1), dim3(kBlock), kHttpLdsBytes, stream, dbox, first_seq);
-  }
-  return hipGetLastError();
+  return launch_kafka_resident(dbox, first_seq, kind, qhdr, stream);
 }
 
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena, uint64_t arena_bytes,

@@ -118,13 +118,11 @@ def test_batcher_destroy_with_calls_in_flight(gpu):
         assert e.value.code == L.L7M_EINVAL
 
 
-def test_batcher_resident_evaluator_relaunch_and_rule_switch(gpu):
-    """The batcher's resident HTTP evaluator (one workgroup polling a pinned
-    mailbox, l7m_kernels.hip http_resident_kernel): verdicts equal the
-    oracle's across its idle exit and relaunch (> 20 ms without batches), a
-    switch to a program of the other instantiation (7 value DFAs: 8-register
-    end codes), to one it cannot serve (back-references: slow path, normal
-    launches) and back, with 8 threads calling concurrently."""
+def test_batcher_idle_gap_and_rule_switches(gpu):
+    """HTTP through the batcher with 8 threads calling concurrently: verdicts
+    equal the oracle's across an idle gap, switches between programs of the
+    4- and 8-register instantiations (7 value DFAs), one with back-references
+    (slow-path second kernel) and back."""
     import threading
     import time
     import numpy as np
