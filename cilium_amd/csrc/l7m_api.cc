@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -53,6 +54,8 @@ int finish_compile(CompileResult&& cr, uint32_t proto, l7m_ruleset** out, char* 
   *out = rs;
   return L7M_OK;
 }
+
+std::atomic<int> g_resident_cus[64];  // resident workgroups running per device (l7m_batch.cc)
 
 int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
   int dev = 0;
@@ -205,6 +208,14 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
   int cus = 0;
   int rc = device_program(rs, &dprog, &cus);
   if (rc != L7M_OK) return rc;
+  {
+    // resident batcher workgroups each hold a CU: a persistent grid sized to
+    // every CU would leave its last workgroup waiting for another to finish
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const int busy = dev >= 0 && dev < 64 ? g_resident_cus[dev].load(std::memory_order_relaxed) : 0;
+    if (busy > 0) cus = cus - busy > 1 ? cus - busy : 1;
+  }
   hipError_t e;
   if (rs->proto == L7M_PROTO_HTTP) {
     if (ids) return L7M_EINVAL;  // HTTP records carry their remote identity
@@ -396,6 +407,10 @@ namespace l7m {
 // The batcher's resident evaluator (l7m_batch.cc): whether the rule set can
 // be served by kafka_resident_kernel, with its device program, instantiation,
 // record stage and serial.
+void resident_running(int dev, int delta) {
+  if (dev >= 0 && dev < 64) g_resident_cus[dev].fetch_add(delta, std::memory_order_relaxed);
+}
+
 bool resident_program(l7m_ruleset* rs, const uint32_t** dprog, int* kind, uint32_t* stage, uint64_t* serial) {
   // Kafka only: for HTTP the launch per batch measured faster (config 2, 8
   // callers: 165 k/s at p50 47 us launched vs 158 k/s at p50 51 us resident,

@@ -46,6 +46,7 @@
 
 namespace l7m {
 bool resident_program(l7m_ruleset* rs, const uint32_t** dprog, int* kind, uint32_t* stage, uint64_t* serial);
+void resident_running(int dev, int delta);  // persistent grids leave those CUs out (l7m_api.cc)
 }
 
 namespace {
@@ -208,6 +209,8 @@ struct l7m_batcher {
     if (res.box) {
       __atomic_store_n(&res.box->quit, 1ull, __ATOMIC_RELEASE);
       if (res.running && res.end) (void)hipEventSynchronize(res.end);
+      if (res.running) l7m::resident_running(device, -1);
+      res.running = false;
     }
     for (l7m_ruleset* r : res.held) l7m_release(r);
     res.held.clear();
@@ -220,6 +223,7 @@ struct l7m_batcher {
   void resident_reap_locked() {
     if (res.running && __atomic_load_n(&res.box->exited, __ATOMIC_ACQUIRE)) {  // it reads no program any more
       res.running = false;
+      l7m::resident_running(device, -1);
       for (l7m_ruleset* r : res.held) l7m_release(r);
       res.held.clear();
     }
@@ -235,6 +239,7 @@ struct l7m_batcher {
         hipEventRecord(res.end, res.stream) != hipSuccess)
       return false;
     res.running = true;
+    l7m::resident_running(device, 1);
     for (uint64_t q = first; q <= res.posted; ++q) resident_hold_locked(res.slot_rs[q % l7m::kResidentSlots]);
     return true;
   }
