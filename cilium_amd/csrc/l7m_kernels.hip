@@ -1162,6 +1162,20 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
                                              reinterpret_cast<uintptr_t>(stg + it * 1024u)),
                                          16, 0, 2);
     }
+    // L2 prefetch of the first lines of the records this tile's lanes will
+    // read from HBM (the lanes past the staged run): 4-byte LDS-DMA loads
+    // into a scratch corner at the end of the stage (config 5: 0.555 ->
+    // 0.545 ms, profiles/r04/ab_round4.md; no effect where tiles are staged)
+    if (t.take > t.k && t.bytes + 256u <= stage) {
+      const bool hbm = lane >= t.k && lane < t.take;
+      const uint64_t o = t.o & ~3ull, len = t.onext > t.o ? t.onext - t.o : 0;
+      auto* junk = reinterpret_cast<__attribute__((address_space(3))) void*>(
+          reinterpret_cast<uintptr_t>(stg + stage - 256u));
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j)
+        if (hbm && 128ull * j < len && o + 128ull * j + 4 <= arena_bytes)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(arena + o + 128ull * j), junk, 4, 0, 0);
+    }
   };
   uint64_t o1, n1, o2, n2;
   load_offs(n * gw / nw, &o1, &n1);
