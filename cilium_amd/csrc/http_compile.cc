@@ -705,7 +705,10 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   for (uint32_t k = 0; k < ndt; ++k) order[k] = k;
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hotness(a) < hotness(b); });
   for (uint32_t k : order) {
-    if (dd[k].kind == kDfaSearch) continue;  // search automata are walked from the program
+    if (dd[k].kind == kDfaSearch) {  // walked from the program; the 256-byte class map in LDS when it fits
+      if (img + 64 <= budget) dd[k].lds_table = img_take(64);
+      continue;
+    }
     const PackedDfa& d = *all[k].d;
     const uint64_t half_es = (d.n_slots + 1) / 2, half_latch = (d.latch.size() + 1) / 2;
     const uint64_t need = ((d.n_slots + 3) & ~3ull) + ((half_es + 3) & ~3ull) + ((half_latch + 3) & ~3ull);
@@ -881,6 +884,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       std::memcpy(P + dd[k].table_off, sd.table.data(), sd.table.size() * 4ull);
       std::memcpy(P + dd[k].es_off, sd.endmask.data(), sd.endmask.size() * 4ull);
       std::memcpy(P + dd[k].acc_cmap_off, sd.cmap, 256);
+      if (dd[k].lds_table != kNone) std::memcpy(I + dd[k].lds_table, sd.cmap, 256);
       std::memcpy(P + dd[k].acc_mid_off, sd.midmask.data(), sd.midmask.size() * 4ull);
     } else {
       std::memcpy(P + dd[k].table_off, d.table.data(), d.n_slots * 4ull);

@@ -52,6 +52,13 @@ typedef __attribute__((address_space(1))) const uint32_t* gptr_u32;
 typedef __attribute__((address_space(3))) const uint32_t* lptr_u32;
 __device__ __forceinline__ uint32_t gld(const uint32_t* p) { return *(gptr_u32)(p); }
 __device__ __forceinline__ uint32_t lld(const uint32_t* p) { return *(lptr_u32)(p); }
+// Byte i of a search automaton's class map: its LDS copy (lds: image byte
+// address) or the program's (explicit address spaces: no flat load).
+__device__ __forceinline__ uint32_t cmap_byte(uint32_t lds, const uint8_t* g, uint32_t i) {
+  if (lds != kNone) return *reinterpret_cast<__attribute__((address_space(3))) const uint8_t*>(
+                        static_cast<uintptr_t>(lds + i));
+  return *(__attribute__((address_space(1))) const uint8_t*)(g + i);
+}
 // A program load whose wait is placed right here (in the branch that needs
 // it): the verification phase runs after the next tile's bytes were
 // requested, and a wait the compiler puts at a later join would be vmcnt(0)
@@ -454,11 +461,12 @@ __device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd,
                                                 uint32_t len) {
   const uint32_t* __restrict__ T = c.prog + dd.table_off;
   const uint8_t* __restrict__ cm = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
+  const uint32_t cml = dd.lds_table != kNone ? 4u * dd.lds_table : kNone;  // class map in LDS (image byte address)
   const uint32_t* __restrict__ mid = c.prog + dd.acc_mid_off;
   const uint32_t ncls = dd.acc_ncls;
   uint32_t st = dd.start_base, acc = dd.start_es8;
   for (uint32_t k = 0; k < len; ++k) {
-    const uint32_t e = gld(T + st * ncls + cm[src.byte(pos + k)]);
+    const uint32_t e = gld(T + st * ncls + cmap_byte(cml, cm, src.byte(pos + k)));
     st = e & 0xffffffu;
     acc |= gld(mid + (e >> 24));
   }
@@ -475,12 +483,13 @@ __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t
   const uint32_t* T[4];
   const uint8_t* cm[4];
   const uint32_t* mid[4];
-  uint32_t ncls[4], st[4], acc[4];
+  uint32_t ncls[4], st[4], acc[4], cml[4];
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
     const DfaDesc& dd = c.dds[d0 + (j < m ? j : 0u)];
     T[j] = c.prog + dd.table_off;
     cm[j] = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
+    cml[j] = dd.lds_table != kNone ? 4u * dd.lds_table : kNone;
     mid[j] = c.prog + dd.acc_mid_off;
     ncls[j] = dd.acc_ncls;
     st[j] = dd.start_base;
@@ -491,7 +500,7 @@ __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
       if (j < m) {
-        const uint32_t e = gld(T[j] + st[j] * ncls[j] + cm[j][b]);
+        const uint32_t e = gld(T[j] + st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b));
         st[j] = e & 0xffffffu;
         acc[j] |= gld(mid[j] + (e >> 24));
       }
