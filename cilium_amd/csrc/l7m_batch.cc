@@ -179,7 +179,7 @@ struct l7m_batcher {
     uint64_t posted = 0;
     std::vector<l7m_ruleset*> held;    // programs the running instance may have read (kept alive until it ends)
     l7m_ruleset* slot_rs[l7m::kResidentSlots] = {};  // rule set of each posted slot
-    bool ok = false;
+    std::atomic<bool> ok{false};
   } res;
   // (res.mu held)
   void resident_hold_locked(l7m_ruleset* r) {
@@ -236,8 +236,12 @@ struct l7m_batcher {
         __atomic_load_n(&res.box->slots[first % l7m::kResidentSlots].kind, __ATOMIC_ACQUIRE));
     __atomic_store_n(&res.box->exited, 0ull, __ATOMIC_RELEASE);
     if (l7m::launch_resident(res.dbox, first, kind, res.qhdr, res.stream) != hipSuccess ||
-        hipEventRecord(res.end, res.stream) != hipSuccess)
+        hipEventRecord(res.end, res.stream) != hipSuccess) {
+      // no workgroup will take the posted slots: stop using the resident path
+      // (their callers get L7M_EDEVICE; later batches are launched)
+      res.ok = false;
       return false;
+    }
     res.running = true;
     l7m::resident_running(device, 1);
     for (uint64_t q = first; q <= res.posted; ++q) resident_hold_locked(res.slot_rs[q % l7m::kResidentSlots]);
