@@ -270,3 +270,14 @@ def test_verification_masks_match_candidate_tables(cfg, n_rules):
     for f, fd in enumerate(P.fields):
         assert bool(pres >> f & 1) == (fd[3] > 0), f
     assert cand != 0
+
+
+def test_nul_and_high_bytes_in_fields_interpreter():
+    """The program interpreter (LDS image encoding: zero dead row, byte-address
+    rows) on fields with NUL and high bytes equals std::regex."""
+    import raw_cases
+    rules, arena, offs = raw_cases.nul_high_byte_case(1500)
+    exp = HttpOracle(rules).eval(arena, offs)
+    got = HttpProgram(L.RuleSet.compile_http(rules).program()).eval(arena, offs)
+    assert np.array_equal(got, exp)
+    assert (exp >= 0).any() and (exp == -1).any()

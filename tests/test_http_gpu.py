@@ -226,3 +226,15 @@ def test_end_code_storage_and_header_jobs(gpu, n_fields):
     assert (rs.info.n_dfas <= 4) == (n_fields == 1) and (rs.info.n_dfas > 8) == (n_fields == 8)
     v = _check(rules, arena, offs, hits=True)
     assert (v >= 0).any() and (v == -1).any()
+
+
+
+def test_nul_and_high_bytes_in_fields(gpu):
+    """Fields holding NUL and high bytes (the LDS walk's dead row is the zero
+    row at image address 0, reached by a byte-3 address fold: a NUL byte after
+    a dead transition must keep the walk dead, a 0xff byte must not alias):
+    verdicts equal std::regex's on random byte strings."""
+    import raw_cases
+    rules, arena, offs = raw_cases.nul_high_byte_case(4000)
+    got = _check(rules, arena, offs)
+    assert (got >= 0).any() and (got == -1).any()
