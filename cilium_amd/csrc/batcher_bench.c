@@ -176,7 +176,7 @@ int main(int argc, char** argv) {
     o.struct_size = sizeof o;
     o.max_batch = 65536;
     o.max_delay_us = 200;
-    o.in_flight = 2;
+    o.in_flight = getenv("L7M_IN_FLIGHT") ? (uint32_t)atoi(getenv("L7M_IN_FLIGHT")) : 2;
     o.eager = (uint32_t)eager;
     if ((rc = l7m_batcher_create(rs, &o, &g_b))) return 1;
     g_threads = T;
@@ -216,12 +216,12 @@ int main(int argc, char** argv) {
       free(args[t].lat);
     }
     qsort(all, done, sizeof(float), cmpf);
-    printf("{\"threads\": %d, \"eager\": %d, \"verdicts_per_s\": %.1f, \"p50_us\": %.1f, \"p99_us\": %.1f, "
+    printf("{\"threads\": %d, \"in_flight\": %u, \"eager\": %d, \"verdicts_per_s\": %.1f, \"p50_us\": %.1f, \"p99_us\": %.1f, "
            "\"max_us\": %.1f, \"batches\": %llu, \"mean_batch\": %.1f, \"requests\": %llu, \"mismatches\": %llu, "
            "\"phases_us\": {\"fill\": %.2f, \"launch\": %.2f, \"gpu\": %.2f, \"wake\": %.2f}, "
            "\"resident\": {\"batches\": %llu, \"rounds\": %llu, \"read_us\": %.2f, \"eval_us\": %.2f, \"sync_us\": %.2f}, "
            "\"cgroup_nr_throttled\": %lld, \"cgroup_throttled_usec\": %lld}\n",
-           T, eager, done / dt, done ? all[done / 2] : 0.0, done ? all[(uint64_t)(done * 0.99)] : 0.0,
+           T, o.in_flight, eager, done / dt, done ? all[done / 2] : 0.0, done ? all[(uint64_t)(done * 0.99)] : 0.0,
            done ? all[done - 1] : 0.0, (unsigned long long)(b1 - b0),
            (b1 - b0) ? (double)(r1 - r0) / (double)(b1 - b0) : 0.0, (unsigned long long)done,
            (unsigned long long)bad, pf.fill_us, pf.launch_us, pf.gpu_us, pf.wake_us,

@@ -367,8 +367,9 @@ struct l7m_batcher {
         }
         continue;
       }
+      const int64_t first = b->first_ns.load();  // 0 until the first caller has stamped it
       if (!eager && !stop.load() && cnt0 < max_batch && !b->want_close.load() &&
-          now_ns() - b->first_ns.load() < static_cast<int64_t>(max_delay_us) * 1000) {
+          (first == 0 || now_ns() - first < static_cast<int64_t>(max_delay_us) * 1000)) {
         cpu_relax();
         continue;
       }
@@ -427,7 +428,8 @@ struct l7m_batcher {
       l7m_release(r);
       batches.fetch_add(1);
       requests.fetch_add(cnt);
-      fill_ns.fetch_add(static_cast<uint64_t>(t_close - b->first_ns.load()));
+      const int64_t t_first = b->first_ns.load();
+      fill_ns.fetch_add(t_close > t_first ? static_cast<uint64_t>(t_close - t_first) : 0);
       launch_ns.fetch_add(static_cast<uint64_t>(t_launch - t_close));
       gpu_ns.fetch_add(static_cast<uint64_t>(t_done - t_launch));
       b->rc = rc;
@@ -480,6 +482,7 @@ struct l7m_batcher {
     Batch* b;
     uint32_t idx;
     uint64_t off;
+    const int64_t t_arrive = now_ns();  // stamped before the reservation, so never after the close
     for (;;) {
       b = cur.load(std::memory_order_acquire);
       uint64_t s = b->resv.load(std::memory_order_acquire);
@@ -500,7 +503,7 @@ struct l7m_batcher {
         break;
       }
     }
-    if (idx == 0) b->first_ns.store(now_ns());
+    if (idx == 0) b->first_ns.store(t_arrive);
     if (len) std::memcpy(b->arena + off, rec, len);
     if (padded != len) std::memset(b->arena + off + len, 0, padded - len);
     b->offs[idx] = off;
