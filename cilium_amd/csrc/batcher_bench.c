@@ -176,7 +176,7 @@ int main(int argc, char** argv) {
     o.struct_size = sizeof o;
     o.max_batch = 65536;
     o.max_delay_us = 200;
-    o.in_flight = getenv("L7M_IN_FLIGHT") ? (uint32_t)atoi(getenv("L7M_IN_FLIGHT")) : 2;
+    o.in_flight = getenv("L7M_IN_FLIGHT") ? (uint32_t)atoi(getenv("L7M_IN_FLIGHT")) : 0;  /* 0: the library default (4) */
     o.eager = (uint32_t)eager;
     if ((rc = l7m_batcher_create(rs, &o, &g_b))) return 1;
     g_threads = T;

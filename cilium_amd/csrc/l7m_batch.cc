@@ -141,7 +141,7 @@ struct Batch {
 struct l7m_batcher {
   uint32_t max_batch = 65536;
   uint32_t max_delay_us = 200;
-  uint32_t in_flight = 2;
+  uint32_t in_flight = 4;
   bool eager = false;
   int device = 0;
   size_t arena_cap = 16u << 20;
@@ -158,7 +158,7 @@ struct l7m_batcher {
   std::condition_variable idle_cv;
   std::vector<std::thread> flushers;
   // statistics (l7m_batcher_stats / l7m_batcher_get_profile)
-  std::atomic<uint64_t> batches{0}, requests{0}, fill_ns{0}, launch_ns{0}, gpu_ns{0}, wake_ns{0};
+  std::atomic<uint64_t> batches{0}, requests{0}, fill_ns{0}, fill_batches{0}, launch_ns{0}, gpu_ns{0}, wake_ns{0};
   std::atomic<uint64_t> res_batches{0}, res_read{0}, res_eval{0}, res_sync{0};  // device ticks (100 MHz)
 
   // Resident evaluator (l7m_kafka.hip kafka_resident_kernel): Kafka batches
@@ -376,7 +376,10 @@ struct l7m_batcher {
       uint64_t s;
       {
         std::lock_guard<std::mutex> g(close_mu);
-        if (cur.load() != b) continue;  // another flusher took it
+        // another flusher took it; or b was taken, recycled and is current again
+        // but still empty (s0 came from its previous use): closing it would
+        // evaluate nothing and strand the batch outside the pool
+        if (cur.load() != b || count_of(b->resv.load()) == 0) continue;
         Batch* nb = fresh();
         if (!nb) {  // out of pinned memory: evaluate what is there, keep filling b's successor later
           std::this_thread::sleep_for(std::chrono::microseconds(100));
@@ -429,7 +432,10 @@ struct l7m_batcher {
       batches.fetch_add(1);
       requests.fetch_add(cnt);
       const int64_t t_first = b->first_ns.load();
-      fill_ns.fetch_add(t_close > t_first ? static_cast<uint64_t>(t_close - t_first) : 0);
+      if (t_first > 0 && t_close > t_first) {  // a batch without its stamp is left out of the fill phase
+        fill_ns.fetch_add(static_cast<uint64_t>(t_close - t_first));
+        fill_batches.fetch_add(1);
+      }
       launch_ns.fetch_add(static_cast<uint64_t>(t_launch - t_close));
       gpu_ns.fetch_add(static_cast<uint64_t>(t_done - t_launch));
       b->rc = rc;
@@ -611,7 +617,8 @@ int l7m_batcher_get_profile(l7m_batcher* b, l7m_batcher_profile* out) {
   const uint64_t nb = b->batches.load(), nr = b->requests.load();
   out->batches = nb;
   out->requests = nr;
-  out->fill_us = nb ? b->fill_ns.load() / 1e3 / nb : 0.0;
+  const uint64_t nf = b->fill_batches.load();
+  out->fill_us = nf ? b->fill_ns.load() / 1e3 / nf : 0.0;
   out->launch_us = nb ? b->launch_ns.load() / 1e3 / nb : 0.0;
   out->gpu_us = nb ? b->gpu_ns.load() / 1e3 / nb : 0.0;
   const uint64_t rb = b->res_batches.load();

@@ -370,7 +370,7 @@ typedef struct {
   uint32_t max_batch;    /* requests per evaluation (0 = 65536)             */
   uint32_t max_delay_us; /* longest wait of a batch's first request (0 = 200) */
   int32_t device;        /* HIP device the batches run on                   */
-  uint32_t in_flight;    /* batches evaluated concurrently (0 = 2, max 8)   */
+  uint32_t in_flight;    /* batches evaluated concurrently (0 = 4, max 8)   */
   uint32_t eager;        /* 1: a free flusher takes the pending requests at
                             once (batch size follows the load; max_delay_us
                             unused); 0: wait for max_batch / max_delay_us  */
