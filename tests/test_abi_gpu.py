@@ -172,4 +172,9 @@ def test_batcher_idle_gap_and_rule_switches(gpu):
     for rs, recs, exp in ((rs_b, recs_b, exp_b), (rs_c, recs_c, exp_c), (rs_a, recs_a, exp_a), (rs_b, recs_b, exp_b)):
         b.set_ruleset(rs)
         run(recs, exp)
+    # every request was counted once, and every batch carried its first request's stamp
+    # (an empty batch closed from a stale pointer showed as a fill phase of ~10^6 us)
+    p = b.profile()
+    assert p["requests"] == 3 * len(recs_a) + 2 * len(recs_b) + len(recs_c)
+    assert 1 <= p["batches"] <= p["requests"] and 0.0 <= p["fill_us"] < 1e5
     b.close()
