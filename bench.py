@@ -73,6 +73,14 @@ def parse():
                     help="HTTP regex dialect: envoy = std::regex full match (the reference as deployed, default); "
                          "re2 = Go regexp MatchString (BASELINE.json's wording; RE2 semantics, not run against Go)")
     ap.add_argument("--parity-sample", type=int, default=200_000, help="requests of the timed batch checked")
+    ap.add_argument("--single-process", action="store_true",
+                    help="N GPUs from ONE process through the library's device set (l7m_multi_eval_device: byte-"
+                         "balanced shards, one stream per GPU, RCCL counter all-reduce) instead of one process per GPU")
+    ap.add_argument("--devices", default=None,
+                    help="--single-process device list, e.g. 0,1,2,3 (default: 0..N-1; 0,0 = two shards on one GPU)")
+    ap.add_argument("--extended", action="store_true",
+                    help="config 2 with workloads.EXTENDED_RULES (\\b, look-ahead, back-references) in front of its "
+                         "1000 rules: the slow pass (http_slow_kernel) decides the requests they may match")
     return ap.parse_args()
 
 
@@ -92,7 +100,7 @@ def host_cores():
     return {"affinity": aff, "nproc": os.cpu_count(), "cgroup_quota_cores": quota, "usable": usable}
 
 
-def cpu_baseline(cfg, rules, seconds, threads, dialect=L.DIALECT_ENVOY_ECMA_FULL):
+def cpu_baseline(cfg, rules, seconds, threads, dialect=L.DIALECT_ENVOY_ECMA_FULL, n_rules=None):
     """Oracle (the reference algorithm restated: per-request linear rule scan,
     std::regex_match per matcher; K4 coverage for Kafka) timed on the host on a
     bounded sample, on `threads` threads (all the host cores this process may
@@ -111,7 +119,7 @@ def cpu_baseline(cfg, rules, seconds, threads, dialect=L.DIALECT_ENVOY_ECMA_FULL
     n0 = 20_000 if cfg != 5 else 16 * threads
 
     def sample(start, n):
-        return W.requests(cfg, start, n, n_rules=len(rules), threads=min(threads, 64))
+        return W.requests(cfg, start, n, n_rules=n_rules or len(rules), threads=min(threads, 64))
 
     # calibrate on a small sample, then size the timed sample to ~`seconds`
     a, o = sample(10_000_000, n0)
@@ -274,6 +282,8 @@ def main():
     dev = torch.device("cuda", gpu)
     cfg = args.config
     scaling = args.scaling or ("strong" if cfg == 4 else "weak")
+    if args.single_process:
+        return run_single_process(args, scaling)
     if cfg == 4:
         return run_mixed(args, world, rank, dev, scaling)
     c = W.CONFIGS[cfg]
@@ -281,6 +291,10 @@ def main():
     n_job = (args.requests or c["n_requests"]) * (world if scaling == "weak" else 1)
 
     rules = W.rules(cfg)
+    if args.extended:
+        if cfg != 2:
+            raise SystemExit("--extended applies to config 2")
+        rules = list(W.EXTENDED_RULES) + rules  # requests still come from config 2's 1000-rule generator
     dialect = L.DIALECT_RE2_SEARCH if args.dialect == "re2" else L.DIALECT_ENVOY_ECMA_FULL
     if dialect != L.DIALECT_ENVOY_ECMA_FULL and c["proto"] != L.PROTO_HTTP:
         raise SystemExit("--dialect applies to HTTP configurations")
@@ -363,7 +377,7 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": (METRIC if cfg == 2 and dialect == L.DIALECT_ENVOY_ECMA_FULL else
+            "metric": (METRIC if cfg == 2 and dialect == L.DIALECT_ENVOY_ECMA_FULL and not args.extended else
                        f"L7 verdicts/sec ({c['name']}{', RE2 MatchString dialect' if dialect else ''}) + achieved "
                        f"HBM GB/s vs peak"),
             "value": value,
@@ -377,7 +391,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic generator libl7gen.so, SURVEY.md §8(d))",
-            "config": {"workload": c["name"] + ("-re2" if dialect else ""), "baseline_config": cfg,
+            "config": {"workload": c["name"] + ("-re2" if dialect else "") + ("+extended10" if args.extended else ""),
+                       "baseline_config": cfg,
                        "dialect": ("re2-search (Go regexp MatchString semantics; RE2 semantics, not run against Go)"
                                    if dialect else "envoy-ecma-full (std::regex_match, the reference as deployed)"),
                        "n_rules": len(rules),
@@ -389,7 +404,8 @@ def main():
                        "dfa_groups": int(rs.info.n_dfas), "dfa_states": int(rs.info.total_dfa_states)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
-                         "traffic": measured_traffic(cfg) if not args.requests and not dialect else None,
+                         "traffic": (measured_traffic(cfg) if not args.requests and not dialect and not args.extended
+                                     else None),
                          "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_launch": alg_bytes},
             "counters_ok": hits_total == expect_hits,
             "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
@@ -399,22 +415,92 @@ def main():
             log("parity sample (oracle, outside the timed region)")
             res["parity"] = parity_leg(cfg, rules, d_verd.cpu().numpy(), lo, per_gpu,
                                        args.threads or host_cores()["usable"], n_sample=args.parity_sample,
-                                       dialect=dialect)
+                                       dialect=dialect, n_rules=c["n_rules"])
             log(f"parity: {res['parity']['mismatches']} mismatches in {res['parity']['sampled']}")
         if keep_host:
             log("end-to-end (pinned host arena)")
             res["e2e"] = e2e_leg(rs, pinned.numpy(), host_offs, per_gpu)
             del pinned
-        if world == 1 and not args.no_batcher and not args.diag and cfg in (2, 3) and not args.requests and not dialect:
+        if (world == 1 and not args.no_batcher and not args.diag and cfg in (2, 3) and not args.requests and
+                not dialect and not args.extended):
             log("batcher (per-request calls)")
             res["batcher"] = batcher_leg(cfg, args.batcher_seconds)
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds,
-                                               args.threads or host_cores()["usable"], dialect=dialect)
+                                               args.threads or host_cores()["usable"], dialect=dialect,
+                                               n_rules=c["n_rules"])
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_single_process(args, scaling):
+    """--single-process: the job on N GPUs from this one process through the
+    library's device set (include/l7match.h l7m_multi_*): the batch is
+    generated once, cut by l7m_shard_bounds into byte-balanced shards, each
+    shard made resident on its GPU; a step is one l7m_multi_eval_device (all
+    shards' kernels concurrently, one stream per GPU, then one RCCL
+    all-reduce of the counters when the GPUs are distinct)."""
+    cfg = args.config
+    if cfg == 4:
+        raise SystemExit("--single-process: configs 1, 2, 3, 5")
+    c = W.CONFIGS[cfg]
+    devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    N = len(devs)
+    threads = args.threads or max(1, min(16, len(os.sched_getaffinity(0))))
+    n_job = (args.requests or c["n_requests"]) * (N if scaling == "weak" else 1)
+    rules = W.rules(cfg)
+    rs = L.RuleSet.compile_http(rules) if c["proto"] == L.PROTO_HTTP else L.RuleSet.compile_kafka(rules)
+    ds = L.DeviceSet(devs)
+    log(f"single process, devices {devs} (RCCL counters: {ds.uses_rccl}); generating {n_job} requests")
+    arena, offs = W.requests(cfg, 0, n_job, threads=threads)
+    size = arena.nbytes - 64
+    b = L.shard_bounds(offs, size, N)
+    shards, verd = [], []
+    for k, d in enumerate(devs):
+        lo, hi = int(b[k]), int(b[k + 1])
+        a0 = int(offs[lo]) if lo < n_job else size
+        a1 = int(offs[hi]) if hi < n_job else size
+        dv = torch.device("cuda", d)
+        da = torch.zeros(((a1 - a0 + 64 + 15) // 16) * 16, dtype=torch.uint8, device=dv)
+        da[:a1 - a0].copy_(torch.from_numpy(arena[a0:a1]))
+        do = torch.from_numpy((offs[lo:hi] - np.uint64(a0)).view(np.int64)).to(dv)
+        vv = torch.empty(hi - lo, dtype=torch.int32, device=dv)
+        verd.append(vv)
+        shards.append((da, a1 - a0, do, hi - lo, vv))
+    rec_bytes = size
+    del arena
+    hits = np.zeros(rs.n_counters, dtype=np.uint64)
+    for _ in range(args.warmup):
+        ds.eval_device(rs, shards, hits)
+    hits[:] = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ds.eval_device(rs, shards, hits)
+    elapsed = time.perf_counter() - t0
+    got = np.concatenate([v.cpu().numpy() for v in verd])
+    value = n_job * args.steps / elapsed
+    alg = rec_bytes + 12 * n_job + 8 * rs.n_counters
+    res = {
+        "metric": (METRIC if cfg == 2 else f"L7 verdicts/sec ({c['name']}) + achieved HBM GB/s vs peak"),
+        "value": value, "unit": "verdicts/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": scaling,
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (deterministic generator libl7gen.so, SURVEY.md §8(d))",
+        "config": {"workload": c["name"], "baseline_config": cfg, "n_rules": len(rules), "requests_total": n_job,
+                   "devices": devs, "shard_bounds": [int(x) for x in b],
+                   "parallelism": f"single process, {N} shards (l7m_multi_eval_device, "
+                                  f"{'RCCL all-reduce' if ds.uses_rccl else 'host sum'} of {rs.n_counters} counters)"},
+        "roofline": {"bound": "hbm", "achieved": alg / (elapsed / args.steps) / 1e9, "peak": HBM_PEAK_GBPS * len(set(devs)),
+                     "unit": "GB/s", "frac": alg / (elapsed / args.steps) / 1e9 / (HBM_PEAK_GBPS * len(set(devs))),
+                     "traffic": None,
+                     "note": "whole-step wall time (kernels + counter reduce); peak = distinct GPUs x 8 TB/s"},
+        "counters_ok": int(hits.sum()) == n_job * args.steps,
+    }
+    if not args.no_parity:
+        res["parity"] = parity_leg(cfg, rules, got, 0, n_job, threads, n_sample=args.parity_sample)
+    print(json.dumps(res), flush=True)
+    ds.close()
 
 
 def run_mixed(args, world, rank, dev, scaling):

@@ -124,8 +124,10 @@ struct Batch {
   ~Batch() {
     if (host) (void)hipHostFree(host);
   }
+  // A caller holding a stale `cur` snapshot may CAS a slot into this batch as
+  // soon as resv loses its closed bit, so every other field is cleared first
+  // and resv last (release): such a caller then sees done == 0, readers == 0.
   void reset() {
-    resv.store(0);
     written.store(0);
     done.store(0);
     readers.store(0);
@@ -133,6 +135,7 @@ struct Batch {
     want_close.store(0);
     first_ns.store(0);
     rc = L7M_OK;
+    resv.store(0, std::memory_order_release);
   }
 };
 
@@ -177,16 +180,36 @@ struct l7m_batcher {
     hipEvent_t end = nullptr;          // recorded after the running instance
     bool running = false;
     uint64_t posted = 0;
-    std::vector<l7m_ruleset*> held;    // programs the running instance may have read (kept alive until it ends)
+    // programs the workgroup may still read, with the last sequence number
+    // posted with each: released once done_seq has passed it (the workgroup
+    // dereferences a slot's program only while it evaluates that slot)
+    std::vector<std::pair<l7m_ruleset*, uint64_t>> held;
     l7m_ruleset* slot_rs[l7m::kResidentSlots] = {};  // rule set of each posted slot
+    // per slot: the sequence number whose outcome its poster has read; a slot
+    // is posted again only after that (result / stamps are not overwritten
+    // under a poster that has not read them yet)
+    std::atomic<uint64_t> consumed[l7m::kResidentSlots] = {};
     std::atomic<bool> ok{false};
   } res;
   // (res.mu held)
-  void resident_hold_locked(l7m_ruleset* r) {
-    if (std::find(res.held.begin(), res.held.end(), r) == res.held.end()) {
-      l7m_retain(r);
-      res.held.push_back(r);
+  void resident_hold_locked(l7m_ruleset* r, uint64_t seq) {
+    for (auto& h : res.held)
+      if (h.first == r) {
+        h.second = std::max(h.second, seq);
+        return;
+      }
+    l7m_retain(r);
+    res.held.emplace_back(r, seq);
+  }
+  // (res.mu held) release programs no pending slot refers to
+  void resident_trim_locked() {
+    const uint64_t done = __atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE);
+    size_t k = 0;
+    for (auto& h : res.held) {
+      if (h.second <= done) l7m_release(h.first);
+      else res.held[k++] = h;
     }
+    res.held.resize(k);
   }
 
   void resident_init() {
@@ -212,7 +235,7 @@ struct l7m_batcher {
       if (res.running) l7m::resident_running(device, -1);
       res.running = false;
     }
-    for (l7m_ruleset* r : res.held) l7m_release(r);
+    for (auto& h : res.held) l7m_release(h.first);
     res.held.clear();
     if (res.end) (void)hipEventDestroy(res.end);
     if (res.qhdr) (void)hipFree(res.qhdr);
@@ -224,7 +247,7 @@ struct l7m_batcher {
     if (res.running && __atomic_load_n(&res.box->exited, __ATOMIC_ACQUIRE)) {  // it reads no program any more
       res.running = false;
       l7m::resident_running(device, -1);
-      for (l7m_ruleset* r : res.held) l7m_release(r);
+      for (auto& h : res.held) l7m_release(h.first);
       res.held.clear();
     }
   }
@@ -238,13 +261,15 @@ struct l7m_batcher {
     if (l7m::launch_resident(res.dbox, first, kind, res.qhdr, res.stream) != hipSuccess ||
         hipEventRecord(res.end, res.stream) != hipSuccess) {
       // no workgroup will take the posted slots: stop using the resident path
-      // (their callers get L7M_EDEVICE; later batches are launched)
+      // (their callers get L7M_EDEVICE; later batches are launched).  exited
+      // goes back to 1 so flushers spinning on posted slots look again.
       res.ok = false;
+      __atomic_store_n(&res.box->exited, 1ull, __ATOMIC_RELEASE);
       return false;
     }
     res.running = true;
     l7m::resident_running(device, 1);
-    for (uint64_t q = first; q <= res.posted; ++q) resident_hold_locked(res.slot_rs[q % l7m::kResidentSlots]);
+    for (uint64_t q = first; q <= res.posted; ++q) resident_hold_locked(res.slot_rs[q % l7m::kResidentSlots], q);
     return true;
   }
   // Evaluate batch b (cnt records, bytes) on the resident workgroup.
@@ -253,11 +278,18 @@ struct l7m_batcher {
     uint64_t seq;
     {
       std::unique_lock<std::mutex> lk(res.mu);
-      while (res.posted - __atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= l7m::kResidentSlots) {
-        lk.unlock();  // ring full (more flushers than slots): let the workgroup catch up
+      // ring full (more flushers than slots), or the slot's previous poster
+      // has not read its outcome yet: let them catch up
+      while (res.posted - __atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= l7m::kResidentSlots ||
+             (res.posted + 1 > l7m::kResidentSlots &&
+              res.consumed[(res.posted + 1) % l7m::kResidentSlots].load(std::memory_order_acquire) <
+                  res.posted + 1 - l7m::kResidentSlots)) {
+        if (!res.ok) return 1;  // the resident path was turned off meanwhile: normal launches
+        lk.unlock();
         cpu_relax();
         lk.lock();
       }
+      if (!res.ok) return 1;
       seq = ++res.posted;
       l7m::ResidentSlot& sl = res.box->slots[seq % l7m::kResidentSlots];
       auto put = [](uint64_t* f, uint64_t v) { __atomic_store_n(f, v, __ATOMIC_RELAXED); };
@@ -274,7 +306,8 @@ struct l7m_batcher {
       put(&sl.result, 0);
       for (uint64_t& x : sl.stamp) put(&x, 0);
       res.slot_rs[seq % l7m::kResidentSlots] = r;
-      resident_hold_locked(r);
+      resident_trim_locked();
+      resident_hold_locked(r, seq);
       __atomic_store_n(&res.box->post_seq, seq, __ATOMIC_RELEASE);
       resident_reap_locked();
       if (!res.running && !resident_launch_locked()) return L7M_EDEVICE;
@@ -291,13 +324,17 @@ struct l7m_batcher {
         res_eval.fetch_add(st[2] - st[1]);
         res_sync.fetch_add(st[3] - st[2]);
       }
-      return __atomic_load_n(&sl.result, __ATOMIC_ACQUIRE) ? 1 : L7M_OK;
+      const int out = __atomic_load_n(&sl.result, __ATOMIC_ACQUIRE) ? 1 : L7M_OK;
+      res.consumed[seq % l7m::kResidentSlots].store(seq, std::memory_order_release);  // the slot may be posted again
+      return out;
     };
     for (uint32_t spin = 0;; ++spin) {
       if (__atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= seq) return outcome();
-      if ((spin & 63) == 63 && __atomic_load_n(&res.box->exited, __ATOMIC_ACQUIRE)) {  // idle exit / other kind
+      if ((spin & 63) == 63 && (__atomic_load_n(&res.box->exited, __ATOMIC_ACQUIRE) || !res.ok)) {
+        // idle exit / other kind / a failed launch
         std::lock_guard<std::mutex> g(res.mu);
         if (__atomic_load_n(&res.box->done_seq, __ATOMIC_ACQUIRE) >= seq) return outcome();
+        if (!res.ok) return L7M_EDEVICE;  // no workgroup will take this slot
         resident_reap_locked();
         if (!res.running && !resident_launch_locked()) return L7M_EDEVICE;
       }

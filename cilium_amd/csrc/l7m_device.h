@@ -29,6 +29,25 @@ inline hipError_t set_lds_attr_once(const void* fn, uint32_t bytes) {
   return e;
 }
 
+// Stream-ordered scratch (hipMallocAsync: the slow pass's executor stacks,
+// the search programs' code columns) comes from the device's default pool;
+// keep its memory mapped between launches instead of returning it at every
+// synchronisation (release threshold 0 by default), once per device.
+inline void keep_stream_pool() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  static std::mutex mu;
+  static std::set<int> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count(dev)) return;
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
+    uint64_t keep = 4ull << 30;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+  done.insert(dev);
+}
+
 // LDS bytes of one HTTP workgroup with `stage` bytes of records per wave, and
 // the stage the LDS leaves after the rule tables (0: the tables do not fit).
 size_t http_lds_bytes(const HttpHeader& h, uint32_t stage);

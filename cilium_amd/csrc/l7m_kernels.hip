@@ -619,6 +619,7 @@ constexpr int32_t kNeedVerify = INT32_MIN;
 // First pass: the request's smallest candidate may be a slow-path rule
 // (kCrSlow): it is queued for http_slow_kernel, which decides it exactly.
 constexpr int32_t kDeferred = INT32_MIN + 1;
+constexpr int32_t kDeferred2 = INT32_MIN + 2;  // slow pass, tier 1 -> tier 2 (regex_vm.h)
 
 // Where field f's value lies in a record (slow pass): the pseudo headers from
 // the fixed part, other fields as the first header whose name maps to f (the
@@ -819,7 +820,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
 // decided by the executor of regex_vm.h on the record's field values (src,
 // vm: this lane's scratch); in the first pass such a rule whose automaton
 // checks pass only marks the request for deferral.
-template <int kReg, bool kSlowPass = false, class Src = GlbSrc>
+template <int kReg, int kSlowPass = 0, class Src = GlbSrc>
 __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h, const WalkOut<kReg>& o,
                                                const Src* src = nullptr, uint32_t* vm = nullptr) {
   const Codes<kReg>& codes = o.codes;
@@ -859,8 +860,9 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
           break;
         }
         const int r = vm_match(c.prog + off, reinterpret_cast<const uint8_t*>(src->w) + pos, len, vm,
-                               kVmScratchWords, kVmMaxSteps);
-        if (r == kVmLimit) min_limit = rid < min_limit ? rid : min_limit;
+                               kSlowPass == 1 ? kVmScratchWords : kVmScratchWords2,
+                               kSlowPass == 1 ? kVmMaxSteps : kVmMaxSteps2);
+        if (r < 0) min_limit = rid < min_limit ? rid : min_limit;  // kVmLimit / kVmDeep
         all = r == kVmMatched;
       }
       if (all) best = rid;
@@ -1018,7 +1020,9 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
   if (h.zero_list.len) scan(h.zero_list);
 
   if (!kSlowPass && min_slow < best) return kDeferred;
-  if (kSlowPass && min_limit < best) return L7M_VERDICT_UNSUPPORTED;  // undecided before the first match
+  // undecided before the first match: the second tier runs it with the large
+  // stack and step budget; past those the verdict is "unsupported"
+  if (kSlowPass && min_limit < best) return kSlowPass == 1 ? kDeferred2 : L7M_VERDICT_UNSUPPORTED;
   if (best != kNone) return static_cast<int32_t>(best);
   // the exact-port entry matched nothing; a port-0 entry without HTTP rules allows
   return h0 ? L7M_VERDICT_DENY : L7M_VERDICT_ALLOW_NO_L7;
@@ -1303,17 +1307,22 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
 // Second pass over the requests the first pass deferred (a slow-path rule may
 // decide them, program.h kCrSlow): one lane per queued request, records read
 // from HBM, the same walk phase, then verification with the slow-path
-// executor (regex_vm.h) on this lane's scratch.  Verdicts and counters of
-// these requests are written here only.
-constexpr uint32_t kSlowBlocks = 2;  // 2048 lanes x kVmScratchWords words (256 MiB) of executor scratch
-template <int kReg, bool kLit>
-__global__ __launch_bounds__(kBlock) void http_slow_kernel(const uint32_t* __restrict__ prog,
-                                                           const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                           const uint64_t* __restrict__ offs, uint64_t n,
-                                                           int32_t* __restrict__ verdicts,
-                                                           unsigned long long* __restrict__ hits,
-                                                           const uint32_t* __restrict__ slowq,
-                                                           uint32_t* __restrict__ vmscratch) {
+// executor (regex_vm.h) on this lane's scratch.  Two tiers (regex_vm.h): tier
+// 1 runs every deferred request on a 32 KiB scratch over one wave per CU;
+// requests it could not decide (stack or step budget) are queued for tier 2,
+// kSlowLanes2 lanes with 1 MiB each.  Verdicts and counters of these requests
+// are written here only.
+constexpr uint32_t kSlowBlock = 64;     // one wave per workgroup (and per CU)
+constexpr uint32_t kSlowBlocks2 = 4;    // tier 2: 256 lanes x 1 MiB
+template <int kReg, bool kLit, int kTier>
+__global__ __launch_bounds__(kSlowBlock) void http_slow_kernel(const uint32_t* __restrict__ prog,
+                                                               const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                               const uint64_t* __restrict__ offs, uint64_t n,
+                                                               int32_t* __restrict__ verdicts,
+                                                               unsigned long long* __restrict__ hits,
+                                                               const uint32_t* __restrict__ slowq,
+                                                               uint32_t* __restrict__ slowq2,
+                                                               uint32_t* __restrict__ vmscratch) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x;
@@ -1321,7 +1330,7 @@ __global__ __launch_bounds__(kBlock) void http_slow_kernel(const uint32_t* __res
   {
     const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
     uint4* l = reinterpret_cast<uint4*>(img);
-    for (uint32_t i = tid; i < h.lds_image_words / 4u; i += kBlock) l[i] = g[i];
+    for (uint32_t i = tid; i < h.lds_image_words / 4u; i += kSlowBlock) l[i] = g[i];
   }
   __syncthreads();
   Ctx c;
@@ -1334,12 +1343,13 @@ __global__ __launch_bounds__(kBlock) void http_slow_kernel(const uint32_t* __res
   c.pool = prog + h.off_pool;
   c.cr = prog + h.off_cr;
   c.remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
-  const uint32_t gtid = blockIdx.x * kBlock + tid;
-  uint32_t* vm = vmscratch + static_cast<uint64_t>(gtid) * kVmScratchWords;
-  const uint32_t nq = slowq[0];
+  const uint32_t gtid = blockIdx.x * kSlowBlock + tid;
+  uint32_t* vm = vmscratch + static_cast<uint64_t>(gtid) * (kTier == 1 ? kVmScratchWords : kVmScratchWords2);
+  const uint32_t* q_in = kTier == 1 ? slowq : slowq2;
+  const uint32_t nq = q_in[0];
   uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t q = gtid; q < nq; q += gridDim.x * kBlock) {
-    const uint32_t ri = slowq[1 + q];
+  for (uint32_t q = gtid; q < nq; q += gridDim.x * kSlowBlock) {
+    const uint32_t ri = q_in[1 + q];
     if (ri >= n) continue;
     const uint64_t o = offs[ri];
     WalkOut<kReg> wo;
@@ -1348,7 +1358,12 @@ __global__ __launch_bounds__(kBlock) void http_slow_kernel(const uint32_t* __res
     const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
     const GlbSrc src{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
     if (inb) v = eval_walk<kReg, 0, kLit>(c, h, src, arena_bytes - o, wo, prof);
-    if (v == kNeedVerify) v = eval_verify<kReg, true>(c, h, wo, &src, vm);
+    if (v == kNeedVerify) v = eval_verify<kReg, kTier>(c, h, wo, &src, vm);
+    if (kTier == 1 && v == kDeferred2) {  // the large-stack tier decides it
+      const uint32_t at = atomicAdd(slowq2, 1u);
+      slowq2[1 + at] = ri;
+      continue;
+    }
     verdicts[ri] = v;
     if (hits && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY)
       atomicAdd(hits + (v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u)), 1ull);
@@ -1388,15 +1403,18 @@ static hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const ui
   return hipGetLastError();
 }
 
-template <int kReg, bool kLit>
-static hipError_t launch_slow(const HttpHeader& h, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
-                              uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                              unsigned long long* hits, const uint32_t* slowq, uint32_t* vmscratch) {
+template <int kReg, bool kLit, int kTier>
+static hipError_t launch_slow(const HttpHeader& h, uint32_t blocks, hipStream_t stream, const uint32_t* dprog,
+                              const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs, uint64_t n,
+                              int32_t* verdicts, unsigned long long* hits, const uint32_t* slowq, uint32_t* slowq2,
+                              uint32_t* vmscratch) {
+  // LDS code columns keep the first pass's stride (Codes<0>: kBlock)
   const size_t lds = 4u * (static_cast<size_t>(h.lds_image_words) + (kReg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock));
-  const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_slow_kernel<kReg, kLit>), kHttpLdsBytes);
+  const hipError_t e =
+      set_lds_attr_once(reinterpret_cast<const void*>(http_slow_kernel<kReg, kLit, kTier>), kHttpLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((http_slow_kernel<kReg, kLit>), dim3(kSlowBlocks), dim3(kBlock), lds, stream, dprog, arena,
-                     arena_bytes, offs, n, verdicts, hits, slowq, vmscratch);
+  hipLaunchKernelGGL((http_slow_kernel<kReg, kLit, kTier>), dim3(blocks), dim3(kSlowBlock), lds, stream, dprog, arena,
+                     arena_bytes, offs, n, verdicts, hits, slowq, slowq2, vmscratch);
   return hipGetLastError();
 }
 
@@ -1450,16 +1468,28 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   // the requests they may decide, http_slow_kernel decides them; the queue
   // (count + up to n indices) and the executor scratch are stream-ordered
   uint32_t* slowq = nullptr;
+  uint32_t* slowq2 = nullptr;
   uint32_t* vms = nullptr;
+  uint32_t* vms2 = nullptr;
   const size_t qbytes = (4ull * (n + 1) + 255) & ~size_t(255);
+  // tier 1: one wave per CU (fewer for small batches), tier 2: kSlowBlocks2 waves
+  const uint64_t waves = (n + kSlowBlock - 1) / kSlowBlock;
+  const uint64_t cus = num_cus > 0 ? static_cast<uint64_t>(num_cus) : 256u;
+  const uint32_t blocks1 = static_cast<uint32_t>(waves < cus ? waves : cus);
+  const uint32_t blocks2 = static_cast<uint32_t>(waves < kSlowBlocks2 ? waves : kSlowBlocks2);
   if (h.n_slow) {
     void* buf = nullptr;
-    const size_t vbytes = static_cast<size_t>(kSlowBlocks) * kBlock * kVmScratchWords * 4u;
-    hipError_t e = hipMallocAsync(&buf, qbytes + vbytes, stream);
+    const size_t v1 = static_cast<size_t>(blocks1) * kSlowBlock * kVmScratchWords * 4u;
+    const size_t v2 = static_cast<size_t>(blocks2) * kSlowBlock * kVmScratchWords2 * 4u;
+    keep_stream_pool();
+    hipError_t e = hipMallocAsync(&buf, 2 * qbytes + v1 + v2, stream);
     if (e == hipSuccess) e = hipMemsetAsync(buf, 0, 4, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(buf) + qbytes, 0, 4, stream);
     if (e != hipSuccess) return e;
     slowq = static_cast<uint32_t*>(buf);
-    vms = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + qbytes);
+    slowq2 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + qbytes);
+    vms = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 2 * qbytes);
+    vms2 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 2 * qbytes + v1);
   }
   hipError_t e = hipSuccess;
 #define L7M_LAUNCH(M, RR)                                                                                          \
@@ -1479,13 +1509,21 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
 #undef L7M_LAUNCH_M
 #undef L7M_LAUNCH
   if (h.n_slow) {
-#define L7M_SLOW(RR)                                                                                              \
-  e = lit ? launch_slow<RR, true>(h, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq, vms)     \
-          : launch_slow<RR, false>(h, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq, vms)
-    if (e == hipSuccess) {
-      if (R == 4) L7M_SLOW(4);
-      else if (R == 8) L7M_SLOW(8);
-      else L7M_SLOW(0);
+#define L7M_SLOW(RR, T, B, V)                                                                                      \
+  e = lit ? launch_slow<RR, true, T>(h, B, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq, slowq2, \
+                                     V)                                                                            \
+          : launch_slow<RR, false, T>(h, B, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq,      \
+                                      slowq2, V)
+    for (int tier = 1; tier <= 2 && e == hipSuccess; ++tier) {
+      if (tier == 1) {
+        if (R == 4) L7M_SLOW(4, 1, blocks1, vms);
+        else if (R == 8) L7M_SLOW(8, 1, blocks1, vms);
+        else L7M_SLOW(0, 1, blocks1, vms);
+      } else {
+        if (R == 4) L7M_SLOW(4, 2, blocks2, vms2);
+        else if (R == 8) L7M_SLOW(8, 2, blocks2, vms2);
+        else L7M_SLOW(0, 2, blocks2, vms2);
+      }
     }
 #undef L7M_SLOW
     const hipError_t e2 = hipFreeAsync(slowq, stream);

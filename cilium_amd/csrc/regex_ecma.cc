@@ -405,6 +405,8 @@ class Parser {
       const unsigned long long k = num_;
       advance();
       if (k < 1 || k >= static_cast<unsigned long long>(groups_)) fail(Status::Syntax, "back-reference");
+      // _M_insert_backref: "referred to an opened sub-expression" (error_backref)
+      for (int g : open_) if (static_cast<unsigned long long>(g) == k) fail(Status::Syntax, "back-reference to an open group");
       Node n;
       n.kind = Node::Backref;
       n.min = static_cast<int>(k);
@@ -427,8 +429,10 @@ class Parser {
     if (tok_ == T_SUB) {  // capture group: numbered by its '(' (_M_insert_subexpr_begin)
       advance();
       const int idx = groups_++;
+      open_.push_back(idx);
       int r = disjunction();
       if (!match(T_SUBEND)) fail(Status::Syntax, "missing )");
+      open_.pop_back();
       Node n;
       n.kind = Node::Group;
       n.min = idx;
@@ -559,6 +563,7 @@ class Parser {
   std::string str_;
   Ast ast_;
   int groups_ = 1;  // capture groups opened so far + 1 (group 0 = the whole match)
+  std::vector<int> open_;  // capture groups whose ')' is still ahead (_M_paren_stack)
 };
 
 // ------------------------------------------------------------------- NFA --
@@ -1188,6 +1193,8 @@ bool has_node(const Ast& a, Node::Kind k) {
 }
 
 namespace {
+constexpr size_t kLowerBudget = 1u << 14;  // nodes of a lowered AST before references stop being copied
+
 // in_ref: copying a group's pattern for a back-reference -- the reference
 // compares text only, so the group's assertions (checked where the group
 // matched) do not apply at the reference's position and are dropped.
@@ -1203,10 +1210,30 @@ int lower_node(const Ast& a, int node, Ast* dst, const std::vector<int>& gnode, 
   switch (n.kind) {
     case Node::Group:
       return lower_node(a, n.kids[0], dst, gnode, exact, drop_look, in_ref);
-    case Node::Backref:
-      // \k matches the text group k captured: a string of group k's language
+    case Node::Backref: {
+      // \k matches the text group k captured: a string of group k's language.
+      // Chained references ((a)(\1\1)(\2\2)...) double the copy per level, so
+      // past kLowerBudget nodes the copy is replaced by [\x00-\xff]* -- still a
+      // superset, and the slow path decides the pattern exactly either way.
       *exact = false;
-      return lower_node(a, a.nodes[gnode[n.min]].kids[0], dst, gnode, exact, drop_look, true);
+      const size_t mark = dst->nodes.size();
+      if (mark < kLowerBudget) {
+        const int r = lower_node(a, a.nodes[gnode[n.min]].kids[0], dst, gnode, exact, drop_look, true);
+        if (dst->nodes.size() <= kLowerBudget) return r;
+        dst->nodes.resize(mark);
+      }
+      Node any;
+      any.kind = Node::Set;
+      any.set.set();
+      dst->nodes.push_back(any);
+      Node star;
+      star.kind = Node::Rep;
+      star.kids = {static_cast<int>(dst->nodes.size()) - 1};
+      star.min = 0;
+      star.max = -1;
+      dst->nodes.push_back(star);
+      return static_cast<int>(dst->nodes.size()) - 1;
+    }
     case Node::Look:
       if (drop_look || in_ref) {
         *exact = false;

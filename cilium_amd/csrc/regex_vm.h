@@ -55,24 +55,33 @@ enum VmFrame : uint32_t {
   kFrLook,         // a = next | neg << 31, b = cur, c = begin; payload: snapshot + previous look frame
 };
 
-// Result of vm_match.
-constexpr int kVmNoMatch = 0, kVmMatched = 1, kVmLimit = -1;
+// Result of vm_match: kVmLimit = the step budget ran out, kVmDeep = the
+// stack (scratch) ran out.
+constexpr int kVmNoMatch = 0, kVmMatched = 1, kVmLimit = -1, kVmDeep = -2;
 // Limits of one evaluation in the HTTP slow pass (and its host restatement in
-// the tests): 128 KiB of state + stack per lane (~8000 four-word frames, one
-// per iteration of a loop over the subject: libstdc++'s recursion needs
-// native frames per step too and overflows its stack at tens of KiB of
-// subject) and 2^22 steps; past either the request's
-// verdict is L7M_VERDICT_UNSUPPORTED.
-constexpr uint32_t kVmScratchWords = 32768;
+// the tests).  Two tiers: every deferred request first runs with 32 KiB of
+// state + stack per lane and 2^22 steps (a few hundred frames cover realistic
+// header values); a request whose evaluation ran out of either runs again with
+// 1 MiB (kVmScratchWords2) and 2^25 steps.  Only past those is its verdict
+// L7M_VERDICT_UNSUPPORTED.  Why 1 MiB: libstdc++'s recursive executor (the
+// reference engine) keeps one native frame per NFA state on the current path,
+// which measured (GCC 11, -O0 / -O2, tests/cpp/regex_stack_probe.cc) >= 11
+// bytes of native stack per byte of this explicit stack on every pattern
+// family probed; a subject that needs more than 1 MiB here needs > 8 MiB of
+// native stack there -- past the 8 MiB default thread stack of an Envoy
+// worker, where std::regex_match overflows.
+constexpr uint32_t kVmScratchWords = 8192;
 constexpr uint32_t kVmMaxSteps = 1u << 22;
+constexpr uint32_t kVmScratchWords2 = 262144;
+constexpr uint32_t kVmMaxSteps2 = 1u << 25;
 
 __host__ __device__ inline bool vm_is_word(uint32_t c) {
   return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '_';
 }
 
-// regex_match(s[0, n), program): kVmMatched / kVmNoMatch, or kVmLimit when
-// the stack (scratch_words) or the step budget ran out -- where libstdc++
-// would recurse past its own stack or run for a very long time.
+// regex_match(s[0, n), program): kVmMatched / kVmNoMatch, kVmDeep when the
+// stack (scratch_words) ran out -- where libstdc++ would recurse deeper --, or
+// kVmLimit when the step budget ran out (where it would run for a long time).
 // scratch: n_caps * 3 + n_reps * 2 words of state, then the stack.
 __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const uint8_t* __restrict__ s, uint32_t n,
                                         uint32_t* __restrict__ scratch, uint32_t scratch_words, uint32_t max_steps) {
@@ -86,7 +95,7 @@ __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const
   uint32_t* rc = rp + nrep;           // repeat: count
   uint32_t* st = rc + nrep;           // the stack
   const uint32_t state_words = 3 * ncap + 2 * nrep;
-  if (state_words + 64 > scratch_words) return kVmLimit;
+  if (state_words + 64 > scratch_words) return kVmDeep;
   const uint32_t cap = scratch_words - state_words;
   for (uint32_t k = 0; k < ncap; ++k) cf[k] = cs[k] = cm[k] = 0;
   for (uint32_t k = 0; k < nrep; ++k) rp[k] = rc[k] = 0;
@@ -150,7 +159,7 @@ __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const
           case kFrRepMore:
             cur = b;
             i = once_more(a, &ok);
-            if (!ok) return kVmLimit;
+            if (!ok) return kVmDeep;
             resumed = i != kVmNone;
             break;
           case kFrRepRestore:
@@ -248,7 +257,7 @@ __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const
       }
       case kVmLook: {  // _M_lookahead: snapshot, fresh repeat counters, prefix search from cur
         const uint32_t size = state_words + 1 + 4;
-        if (sp + size > cap) return kVmLimit;
+        if (sp + size > cap) return kVmDeep;
         uint32_t* snap = st + sp;
         for (uint32_t k = 0; k < ncap; ++k) {
           snap[k] = cf[k];
@@ -320,7 +329,7 @@ __host__ __device__ inline int vm_match(const uint32_t* __restrict__ prog, const
       default:
         return kVmLimit;
     }
-    if (!ok) return kVmLimit;
+    if (!ok) return kVmDeep;
   }
 }
 

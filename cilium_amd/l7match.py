@@ -67,6 +67,8 @@ EXPORTED_SYMBOLS = (
     "l7m_batcher_eval_from", "l7m_proxy_stats_table_create", "l7m_proxy_stats_table_destroy",
     "l7m_proxy_stats_update", "l7m_proxy_stats_get", "l7m_http_access_log", "l7m_kafka_access_log",
     "l7m_kafka_api_key_name", "l7m_batcher_get_profile",
+    "l7m_multi_create", "l7m_multi_destroy", "l7m_multi_uses_rccl", "l7m_shard_bounds", "l7m_multi_eval",
+    "l7m_multi_eval_device",
 )
 
 
@@ -266,6 +268,13 @@ def _load() -> ctypes.CDLL:
     lib.l7m_host_mapped.argtypes = [P, sz]
     lib.l7m_free_pinned.argtypes = [P]
     lib.l7m_free_pinned.restype = None
+    lib.l7m_multi_create.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(P)]
+    lib.l7m_multi_destroy.argtypes = [P]
+    lib.l7m_multi_destroy.restype = None
+    lib.l7m_multi_uses_rccl.argtypes = [P]
+    lib.l7m_shard_bounds.argtypes = [P, sz, sz, ctypes.c_uint32, P]
+    lib.l7m_multi_eval.argtypes = [P, P, P, sz, P, sz, P, P, P, ctypes.c_uint32]
+    lib.l7m_multi_eval_device.argtypes = [P, P, P, P, ctypes.c_uint32]
     return lib
 
 
@@ -698,6 +707,76 @@ class Batcher:
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.l7m_batcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class _Shard(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("arena_bytes", ctypes.c_size_t), ("rec_offsets", ctypes.c_void_p),
+                ("n", ctypes.c_size_t), ("src_identities", ctypes.c_void_p), ("verdicts", ctypes.c_void_p)]
+
+
+def shard_bounds(offsets: np.ndarray, arena_bytes: int, parts: int) -> np.ndarray:
+    """l7m_shard_bounds: byte-balanced contiguous shards, bounds[0..parts]."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    out = np.zeros(parts + 1, dtype=np.uint64)
+    rc = _lib.l7m_shard_bounds(offsets.ctypes.data, offsets.shape[0], int(arena_bytes), parts, out.ctypes.data)
+    if rc != L7M_OK:
+        raise L7Error(rc, "l7m_shard_bounds failed")
+    return out
+
+
+class DeviceSet:
+    """l7m_multi: several GPUs from one process (include/l7match.h) -- byte-
+    balanced shards, one stream per device, counters summed by one RCCL
+    all-reduce over a single-process communicator (or on the host when a
+    device repeats)."""
+
+    def __init__(self, devices: Sequence[int]):
+        arr = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        rc = _lib.l7m_multi_create(arr, len(devices), ctypes.byref(h))
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_multi_create failed")
+        self._h = h
+        self.devices = list(devices)
+
+    @property
+    def uses_rccl(self) -> bool:
+        return bool(_lib.l7m_multi_uses_rccl(self._h))
+
+    def eval(self, rs: "RuleSet", arena: np.ndarray, offsets: np.ndarray, hits: Optional[np.ndarray] = None,
+             identities: Optional[np.ndarray] = None) -> np.ndarray:
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.shape[0]
+        v = np.empty(n, dtype=np.int32)
+        ids = None if identities is None else np.ascontiguousarray(identities, dtype=np.uint32)
+        rc = _lib.l7m_multi_eval(self._h, rs.handle, arena.ctypes.data, arena.nbytes, offsets.ctypes.data, n,
+                                 None if ids is None else ids.ctypes.data, v.ctypes.data,
+                                 None if hits is None else hits.ctypes.data, 0)
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_multi_eval failed")
+        return v
+
+    def eval_device(self, rs: "RuleSet", shards, hits: Optional[np.ndarray] = None, flags: int = 0) -> None:
+        """shards: one (d_arena, arena_bytes, d_offsets, n, d_verdicts[, d_ids]) per device (device pointers
+        as ints or objects with data_ptr())."""
+        ptr = lambda x: None if x is None else (x.data_ptr() if hasattr(x, "data_ptr") else int(x))  # noqa: E731
+        arr = (_Shard * len(shards))()
+        for k, sh in enumerate(shards):
+            a, ab, o, n, v = sh[:5]
+            ids = sh[5] if len(sh) > 5 else None
+            arr[k] = _Shard(ptr(a), ab, ptr(o), n, ptr(ids), ptr(v))
+        rc = _lib.l7m_multi_eval_device(self._h, rs.handle, arr, None if hits is None else hits.ctypes.data, flags)
+        if rc != L7M_OK:
+            raise L7Error(rc, "l7m_multi_eval_device failed")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.l7m_multi_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -26,6 +26,27 @@ CONFIGS = {
 }
 
 
+# HTTP rules with the ECMAScript constructs beyond the regular core that the
+# reference accepts (std::regex via Envoy, envoy/cilium_network_policy.h:52-56;
+# patterns passed verbatim by pkg/envoy/server.go:276-289): word-delimited API
+# versions, "anything but admin", extension filters, repeated path segments.
+# bench.py --extended puts them in front of config 2's rules (indices 0..9, so
+# they decide first); the back-reference rules send every request whose
+# superset automaton matches through the slow pass.
+EXTENDED_RULES = [
+    L.PortRuleHTTP(Path=".*\\bv1\\b.*", Method="GET"),
+    L.PortRuleHTTP(Path="^(?!.*admin).*$", Method="POST"),
+    L.PortRuleHTTP(Path="/files/(?!secret)\\w+(\\.\\w+)?"),
+    L.PortRuleHTTP(Path=".*\\.(?!exe$)\\w+", Method="PUT"),
+    L.PortRuleHTTP(Path="/(?=[a-z]+/)[a-z]+/\\w*\\b"),
+    L.PortRuleHTTP(Method="(?!DELETE)[A-Z]+", Path="/ro/.*"),
+    L.PortRuleHTTP(Host="(?=.*\\.local$)svc\\d+\\..*"),
+    L.PortRuleHTTP(Path="/svc\\d+/v\\d+\\B.*", Headers=["x-tenant: t1"]),
+    L.PortRuleHTTP(Path="/(\\w+)/\\1(/.*)?"),                 # repeated segment (back-reference)
+    L.PortRuleHTTP(Path="/(a|bb)+-\\1"),                      # back-reference after a loop
+]
+
+
 def _load():
     if not os.path.exists(GEN_PATH):
         raise ImportError(f"{GEN_PATH} missing: make -C cilium_amd/csrc")

@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define L7M_ABI_VERSION 3
+#define L7M_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define L7M_OK 0
@@ -74,8 +74,17 @@ extern "C" {
                                         pass's limits (nesting depth 8, slab, queue).
                                         HTTP: a rule with a back-reference / look-around
                                         matcher (slow path, regex_vm.h) ran past the
-                                        executor's step or stack limit before any
-                                        earlier rule decided the request            */
+                                        executor's second-tier limits before any
+                                        earlier rule decided the request: more than
+                                        1 MiB of backtracking stack (262144 words),
+                                        which std::regex_match's recursion turns into
+                                        more than 8 MiB of native stack (>= 8 native
+                                        bytes per executor byte, measured >= 12 on
+                                        every family in tests/test_slow_tiers_cpu.py):
+                                        it overflows an Envoy worker's default thread
+                                        stack there; or more than 2^25 backtracking
+                                        steps (exponential patterns the reference
+                                        spends seconds on)                          */
 #define L7M_VERDICT_ALLOW_NO_L7 (0x7fffffff) /* HTTP rule list empty: port has no L7
                                         rules, Envoy allows (cilium_network_policy.h:129-135) */
 #define L7M_VERDICT_ALLOW_NO_PORT_POLICY (0x7ffffffe) /* no per-port policy for the
@@ -346,6 +355,52 @@ int l7m_eval_device(const l7m_ruleset* rs, const void* d_arena, size_t arena_byt
 int l7m_eval_device_ids(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes,
                         const void* d_rec_offsets, size_t n, const void* d_src_identities,
                         void* d_verdicts, void* d_rule_hits, void* hip_stream, uint32_t flags);
+
+/* ---- several GPUs from one process ----------------
+ * Requests are independent, so a batch is cut into contiguous byte-balanced
+ * shards, one per device, evaluated concurrently (one HIP stream per device,
+ * the program replicated on each), and the per-rule counters are summed with
+ * ONE RCCL all-reduce (ncclAllReduce, uint64 sum) over a single-process
+ * communicator of the devices (ncclCommInitAll).  This is the in-library
+ * form of bench.py's process-per-GPU sharding, for a caller that is one
+ * process: cilium-agent's Kafka proxy calling canAccess
+ * (pkg/proxy/kafka.go:116-152) through cgo, or one Envoy filter instance.
+ * A device may appear more than once (several shards on one GPU); RCCL needs
+ * distinct devices, so such sets (and L7M_MULTI_NO_RCCL=1) sum the counters
+ * on the host instead.  Verdicts and counters equal one l7m_eval over the
+ * whole batch.  Calls on one device set are serialised; distinct sets run
+ * concurrently. */
+typedef struct l7m_multi l7m_multi;
+int l7m_multi_create(const int* devices, uint32_t n_devices, l7m_multi** out);
+void l7m_multi_destroy(l7m_multi* m);
+/* 1 when the set's counters are reduced by RCCL, 0 when on the host. */
+int l7m_multi_uses_rccl(const l7m_multi* m);
+/* Byte-balanced contiguous shards of a packed batch: bounds[0..parts] record
+ * indices (bounds[0] = 0, bounds[parts] = n); shard k = [bounds[k],
+ * bounds[k+1]) holds the records whose arena bytes are closest to k / parts
+ * of the total (cilium_amd/dist.py byte_balanced_bounds).  Offsets must
+ * ascend (what every packer produces): L7M_EINVAL otherwise. */
+int l7m_shard_bounds(const uint64_t* rec_offsets, size_t n, size_t arena_bytes, uint32_t parts,
+                     uint64_t* bounds);
+/* l7m_eval_ids over the device set: host arena cut by l7m_shard_bounds,
+ * each shard copied to its device, verdicts gathered, counters reduced. */
+int l7m_multi_eval(l7m_multi* m, const l7m_ruleset* rs, const uint8_t* arena, size_t arena_bytes,
+                   const uint64_t* rec_offsets, size_t n, const uint32_t* src_identities,
+                   int32_t* verdicts, uint64_t* rule_hits, uint32_t flags);
+/* Device-resident shards (HBM): shard k lives on device k of the set (its
+ * pointers are device pointers there; rec_offsets relative to its arena).
+ * Synchronous: returns after every device's kernels and the counter
+ * all-reduce; rule_hits (host, n_rules + 2) accumulates the job's sum. */
+typedef struct {
+  const void* arena;
+  size_t arena_bytes;
+  const void* rec_offsets;
+  size_t n;
+  const void* src_identities; /* Kafka L7DataMap rule sets, or NULL */
+  void* verdicts;
+} l7m_shard;
+int l7m_multi_eval_device(l7m_multi* m, const l7m_ruleset* rs, const l7m_shard* shards,
+                          uint64_t* rule_hits, uint32_t flags);
 
 /* ---- batching front-end (the call-site shape of the reference) ------------
  * canAccess (pkg/proxy/kafka.go:116-152) and AccessFilter::decodeHeaders

@@ -53,6 +53,9 @@
 #include <unordered_set>
 #include <vector>
 
+#include <pthread.h>
+#include <sys/mman.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include "../include/l7match.h"
@@ -927,6 +930,46 @@ int32_t eval_kafka_one(const KafkaOracle& o, const KReq& q, uint64_t mask = ~0ul
   return L7M_VERDICT_DENY;
 }
 
+// Run f() on a fresh thread whose 1 GiB stack is reserved but not committed,
+// and report how many bytes of it were touched (mincore: the lowest resident
+// page).  That is the native stack the reference engine's recursion needs for
+// this call -- std::regex_match overflows an Envoy worker's 8 MiB default
+// stack exactly when it exceeds that.
+template <class F>
+uint64_t run_on_measured_stack(F&& f) {
+  const size_t sz = 1ull << 30, pg = static_cast<size_t>(sysconf(_SC_PAGESIZE));
+  void* stk = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (stk == MAP_FAILED) return ~0ull;
+  struct Job {
+    F* f;
+    static void* run(void* p) {
+      (*static_cast<Job*>(p)->f)();
+      return nullptr;
+    }
+  } job{&f};
+  pthread_attr_t at;
+  pthread_attr_init(&at);
+  pthread_attr_setstack(&at, stk, sz);
+  pthread_t t;
+  uint64_t used = ~0ull;
+  if (pthread_create(&t, &at, &Job::run, &job) == 0) {
+    pthread_join(t, nullptr);
+    std::vector<unsigned char> res(sz / pg);
+    if (mincore(stk, sz, res.data()) == 0) {
+      size_t lo = res.size();
+      for (size_t k = 0; k < res.size(); ++k)
+        if (res[k] & 1) {
+          lo = k;
+          break;
+        }
+      used = static_cast<uint64_t>(res.size() - lo) * pg;
+    }
+  }
+  pthread_attr_destroy(&at);
+  munmap(stk, sz);
+  return used;
+}
+
 template <class F>
 void parallel_for(size_t n, int threads, F&& f) {
   if (threads <= 1 || n < 2 * static_cast<size_t>(threads)) {
@@ -1088,6 +1131,35 @@ int orc_http_eval(void* h, const uint8_t* arena, size_t arena_bytes, const uint6
 }
 
 void orc_http_free(void* h) { delete static_cast<HttpOracle*>(h); }
+
+// orc_http_eval one request at a time, each on a measured stack: stack_used[i]
+// = native stack bytes the reference's evaluation of request i touched (the
+// rules' matchers in index order, as eval_http_one runs them).
+int orc_http_eval_stack(void* h, const uint8_t* arena, size_t arena_bytes, const uint64_t* offs, size_t n,
+                        int32_t* verdicts, uint64_t* stack_used) {
+  const HttpOracle& o = *static_cast<HttpOracle*>(h);
+  for (size_t i = 0; i < n; ++i) {
+    const HttpReq q = parse_http(arena, arena_bytes, offs[i]);
+    int32_t v = L7M_VERDICT_PARSE_ERROR;
+    stack_used[i] = run_on_measured_stack([&]() { v = eval_http_one(o, q); });
+    verdicts[i] = v;
+  }
+  return L7M_OK;
+}
+
+// std::regex_match(input, pattern) on a measured stack: the result (1 / 0,
+// -1 if the pattern does not compile) and the native stack bytes it touched.
+int orc_regex_match_stack(const char* pattern, const char* input, size_t input_len, uint64_t* stack_used) {
+  int r = -1;
+  try {
+    std::regex re(pattern, std::regex::ECMAScript | std::regex::optimize);
+    const std::string s(input, input_len);
+    *stack_used = run_on_measured_stack([&]() { r = std::regex_match(s, re) ? 1 : 0; });
+  } catch (const std::regex_error&) {
+    r = -1;
+  }
+  return r;
+}
 
 // 0: evaluate every rule's matchers (the reference's per-request loop as
 // Envoy runs it), 1 (default): skip rules the per-rule prefilter rejects.

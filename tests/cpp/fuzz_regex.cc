@@ -90,7 +90,28 @@ int main(int argc, char** argv) {
   g_assert = argc > 4 && atoi(argv[4]) != 0;
   long checked = 0, mism = 0, unsup = 0, rejected = 0, parse_mism = 0, superset = 0, packed_mism = 0;
   long vm_checked = 0, vm_mism = 0, vm_limit = 0;
+  long accept_mism = 0;
   std::vector<uint32_t> scratch(1u << 16);
+  // fixed cases: references to a group that is still open are error_backref
+  // in libstdc++ (_M_insert_backref); chained references must lower in bounded
+  // size (each level doubles a literal copy)
+  {
+    std::string chain = "(a)";
+    for (int k = 1; k < 40; ++k) chain += "(\\" + std::to_string(k) + "\\" + std::to_string(k) + ")";
+    const char* fixed[] = {"(a\\1)", "(a(b\\2))", "(x(y|\\2))", "((a)\\1)", "(a)\\1", "(a)(b\\1)"};
+    for (const char* fp : fixed) {
+      bool sok = true;
+      try { std::regex r(fp, std::regex::ECMAScript); } catch (...) { sok = false; }
+      Ast fa; std::string ferr;
+      const bool pok = parse_ecma(fp, &fa, &ferr) == Status::Ok;
+      if (sok != pok) { ++accept_mism; printf("FIXED-MISMATCH %s std=%d ours=%d\n", fp, sok, pok); }
+    }
+    Ast ca; std::string cerr;
+    if (parse_ecma(chain, &ca, &cerr) != Status::Ok) { ++accept_mism; printf("CHAIN-PARSE %s\n", cerr.c_str()); }
+    bool cex = true;
+    Ast cl = lower_for_dfa(ca, &cex);
+    if (cex || cl.nodes.size() > (1u << 16)) { ++accept_mism; printf("CHAIN-LOWER nodes=%zu\n", cl.nodes.size()); }
+  }
   for (int i = 0; i < npat; ++i) {
     bool qq = false;
     g_groups = 0;
@@ -101,7 +122,14 @@ int main(int argc, char** argv) {
     try { r = std::regex(p, std::regex::ECMAScript | std::regex::optimize); } catch (...) { ok = false; }
     Ast full; std::string err;
     Status st = parse_ecma(p, &full, &err);
-    if (!ok) { rejected++; continue; }
+    if (!ok) {
+      rejected++;
+      if (st == Status::Ok) {  // std::regex rejects what the parser accepted
+        ++accept_mism;
+        if (accept_mism < 20) printf("ACCEPT-MISMATCH %s\n", p.c_str());
+      }
+      continue;
+    }
     if (st == Status::Unsupported) { unsup++; continue; }
     if (st != Status::Ok) { parse_mism++; printf("PARSE-MISMATCH %s : %s\n", p.c_str(), err.c_str()); continue; }
     // the slow path (libstdc++'s executor restated) must equal std::regex on
@@ -171,7 +199,7 @@ int main(int argc, char** argv) {
     }
   }
   printf("checked=%ld mismatches=%ld unsupported=%ld rejected_by_std=%ld parse_mismatch=%ld superset=%ld "
-         "packed_mismatch=%ld vm_checked=%ld vm_mismatch=%ld vm_limit=%ld\n", checked, mism, unsup, rejected,
-         parse_mism, superset, packed_mism, vm_checked, vm_mism, vm_limit);
-  return (mism || parse_mism || packed_mism || vm_mism || vm_limit) ? 1 : 0;
+         "packed_mismatch=%ld vm_checked=%ld vm_mismatch=%ld vm_limit=%ld accept_mismatch=%ld\n", checked, mism, unsup,
+         rejected, parse_mism, superset, packed_mism, vm_checked, vm_mism, vm_limit, accept_mism);
+  return (mism || parse_mism || packed_mism || vm_mism || vm_limit || accept_mism) ? 1 : 0;
 }

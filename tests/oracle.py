@@ -42,6 +42,8 @@ def _load():
     lib.orc_kafka_eval_ids.argtypes = [P, P, sz, P, sz, P, P, ctypes.c_int]
     lib.orc_regex_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
     lib.orc_regex_search.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz]
+    lib.orc_http_eval_stack.argtypes = [P, P, sz, P, sz, P, P]
+    lib.orc_regex_match_stack.argtypes = [ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint64)]
     return lib
 
 
@@ -87,6 +89,23 @@ class HttpOracle:
         _lib.orc_http_eval(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
                            offsets.shape[0], v.ctypes.data, threads)
         return v
+
+    def eval_stack(self, arena, offsets):
+        """(verdicts, native stack bytes each request's evaluation touched):
+        every request on a fresh thread with a 1 GiB reserved stack, so
+        std::regex_match finishes where an 8 MiB thread would overflow."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        v = np.empty(offsets.shape[0], dtype=np.int32)
+        used = np.empty(offsets.shape[0], dtype=np.uint64)
+        _lib.orc_http_eval_stack(self._h, arena.ctypes.data, arena.nbytes, offsets.ctypes.data,
+                                 offsets.shape[0], v.ctypes.data, used.ctypes.data)
+        return v, used
+
+
+# The default stack of a thread (ulimit -s: an Envoy worker's): std::regex_match
+# overflows it (SIGSEGV, the Envoy process dies) past this much recursion.
+ENVOY_THREAD_STACK = 8 << 20
 
 
 class PolicyOracle:
@@ -169,6 +188,13 @@ class KafkaOracle:
 def regex_match(pattern: str, value: bytes) -> int:
     """std::regex_match(value, std::regex(pattern, optimize)) -> 1/0, -1 if invalid."""
     return _lib.orc_regex_match(pattern.encode(), value, len(value))
+
+
+def regex_match_stack(pattern: str, value: bytes):
+    """(std::regex_match result 1/0/-1, native stack bytes it touched)."""
+    used = ctypes.c_uint64(0)
+    r = _lib.orc_regex_match_stack(pattern.encode(), value, len(value), ctypes.byref(used))
+    return r, int(used.value)
 
 
 def regex_search(pattern: str, value: bytes) -> int:

@@ -17,7 +17,11 @@ from cilium_amd import l7match as L
 
 _VM = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "bin", "libvmhost.so"))
 _VM.vm_host_match.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
-VM_SCRATCH_WORDS, VM_MAX_STEPS = 32768, 1 << 22  # regex_vm.h kVmScratchWords / kVmMaxSteps
+# regex_vm.h kVmScratchWords2 / kVmMaxSteps2: the slow pass's second tier (a
+# request the first tier could not decide runs again with these), so the
+# verdict is the one these limits give
+VM_SCRATCH_WORDS, VM_MAX_STEPS = 262144, 1 << 25
+VM_DEEP, VM_LIMIT = -2, -1
 CR_SLOW = 0x40000000  # program.h kCrSlow
 
 KNONE = 0xFFFFFFFF

@@ -7,21 +7,12 @@ oracle is std::regex_match itself (oracle/l7oracle.cc)."""
 import numpy as np
 
 from cilium_amd import l7match as L
+from cilium_amd import workloads as W
 
 # Policies a user could write: word-delimited API versions, "anything but
-# admin", extension filters, repeated path segments.
-REALISTIC = [
-    L.PortRuleHTTP(Path=".*\\bv1\\b.*", Method="GET"),
-    L.PortRuleHTTP(Path="^(?!.*admin).*$", Method="POST"),
-    L.PortRuleHTTP(Path="/files/(?!secret)\\w+(\\.\\w+)?"),
-    L.PortRuleHTTP(Path=".*\\.(?!exe$)\\w+", Method="PUT"),
-    L.PortRuleHTTP(Path="/(?=[a-z]+/)[a-z]+/\\w*\\b"),
-    L.PortRuleHTTP(Method="(?!DELETE)[A-Z]+", Path="/ro/.*"),
-    L.PortRuleHTTP(Host="(?=.*\\.local$)svc\\d+\\..*"),
-    L.PortRuleHTTP(Path="/svc\\d+/v\\d+\\B.*", Headers=["x-tenant: t1"]),
-    L.PortRuleHTTP(Path="/(\\w+)/\\1(/.*)?"),                 # repeated segment (back-reference)
-    L.PortRuleHTTP(Path="/(a|bb)+-\\1"),                      # back-reference after a loop
-]
+# admin", extension filters, repeated path segments (shared with bench.py
+# --extended).
+REALISTIC = list(W.EXTENDED_RULES)
 
 ALPHA = list("ab/.-_xv1exmindEXs0 ")
 

@@ -47,7 +47,7 @@ def test_library_exports_every_header_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True).stdout
     for sym in declared:
         assert re.search(rf"\bT {sym}\b", out), sym
-    assert lib.l7m_abi_version() == 3
+    assert lib.l7m_abi_version() == 4
 
 
 def test_eval_without_device_fails_loudly():

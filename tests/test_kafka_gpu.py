@@ -219,3 +219,44 @@ def test_batcher_kafka_l7datamap_threads(gpu):
     assert not errs, errs
     assert np.array_equal(got, exp)
     assert requests == len(offs) and batches < requests
+
+
+def test_batcher_resident_recycled_batch_new_bytes_same_offsets(gpu):
+    """Round-4 r04f: the resident Kafka evaluator returned −2 (parse error) for
+    a well-formed record after a set_ruleset.  Cause: a batch is pinned,
+    device-mapped host memory that the workgroup reads through the GPU caches;
+    a recycled batch puts new record bytes at the same host addresses, and a
+    workgroup that kept the previous use's lines in L2 read stale bytes (the
+    old record, or a torn mix of two).  The shipped protocol invalidates the
+    L1 / L2 once per resident round before reading the posted batches
+    (l7m_kafka.hip kafka_resident_kernel).  Here one caller alternates
+    records of equal length and different bytes (so every batch reuses the
+    same slot offsets of a recycled batch), across rule-set switches; every
+    verdict must be the oracle's and the resident path must have run."""
+    import kafka_wire as KW
+    topics_a = [f"topic-{i:04d}" for i in range(64)]
+    topics_b = [f"topic-{i + 5000:04d}" for i in range(64)]
+    recs = []
+    for i in range(64):
+        recs.append(KW.produce(1, "client-01", [(topics_a[i], [(0, b"")])]))
+        recs.append(KW.produce(1, "client-01", [(topics_b[i], [(0, b"")])]))
+    assert len({len(r) for r in recs}) == 1
+    rule_sets = [[L.PortRuleKafka(APIKey="produce", Topic=t) for t in topics_a[::2] + topics_b[1::2]],
+                 [L.PortRuleKafka(APIKey="produce", Topic=t) for t in topics_b[::2] + topics_a[1::2]]]
+    arena, offs = L.pack_records(recs)
+    exps = [KafkaOracle(r).eval(arena, offs) for r in rule_sets]
+    assert all((e >= 0).any() and (e == -1).any() for e in exps)
+    rss = [L.RuleSet.compile_kafka(r) for r in rule_sets]
+    b = L.Batcher(rss[0], max_delay_us=50, eager=True)
+    try:
+        for rnd in range(6):
+            k = rnd % 2
+            if rnd:
+                b.set_ruleset(rss[k])
+            got = [b.eval(r) for r in recs]
+            assert got == exps[k].tolist(), (rnd, [(i, g, int(e)) for i, (g, e) in enumerate(zip(got, exps[k]))
+                                                   if g != e][:8])
+        p = b.profile()
+        assert p["resident_batches"] > 0, p
+    finally:
+        b.close()

@@ -11,7 +11,7 @@ import pytest
 import regex_ext_cases as X
 from cilium_amd import l7match as L
 from cilium_amd import workloads as W
-from oracle import HttpOracle
+from oracle import ENVOY_THREAD_STACK, HttpOracle
 from program_interp import HttpProgram
 
 pytestmark = pytest.mark.gpu
@@ -56,15 +56,42 @@ def test_random_extended_rule_sets(gpu):
         _check(rules, arena, offs)
 
 
-def test_slow_path_limits_match_the_host_executor(gpu):
-    """Subjects past the slow path's stack (regex_vm.h kVmScratchWords): the
-    GPU reports L7M_VERDICT_UNSUPPORTED exactly where the host build of the
-    same executor does; short subjects are decided."""
-    rules = [L.PortRuleHTTP(Path="/(a)(?:.)*\\1z"), L.PortRuleHTTP(Path="/.*")]
-    reqs = [L.HTTPRequest("GET", "/a" + "b" * n + "az") for n in (10, 100, 2000, 12000, 40000)]
+def test_slow_path_decides_what_the_reference_decides(gpu):
+    """Long subjects through back-reference rules: the GPU (two-tier slow pass,
+    regex_vm.h) against std::regex_match itself, run by the oracle on a
+    measured 1 GiB stack.  Every request whose reference evaluation fits an
+    8 MiB thread stack (an Envoy worker's) gets the reference's verdict; −3
+    appears only where the oracle measured more than 8 MiB of native stack,
+    i.e. where std::regex_match would overflow the worker and crash Envoy."""
+    rules = [L.PortRuleHTTP(Path="/(a)(?:.)*\\1z"), L.PortRuleHTTP(Path="/(a)(b|c)*\\1z"),
+             L.PortRuleHTTP(Path="/.*")]
+    sizes = (10, 100, 2000, 8000, 12000, 20000, 40000, 60000)
+    reqs = [L.HTTPRequest("GET", "/a" + "b" * n + "az") for n in sizes]
+    reqs += [L.HTTPRequest("GET", "/a" + "b" * n + "ay") for n in sizes]  # rule 2 decides after two failures
+    reqs += [L.HTTPRequest("GET", "/a" + "c" * n + "az") for n in (5000, 20000)]
     arena, offs = L.pack_http(reqs)
     rs = L.RuleSet.compile_http(rules)
     got = rs.eval(arena, offs)
-    exp = HttpProgram(rs.program()).eval(arena, offs)
-    assert got.tolist() == exp.tolist()
-    assert got[:2].tolist() == [0, 0] and L.VERDICT_UNSUPPORTED in got.tolist()
+    exp, used = HttpOracle(rules, prefilter=False).eval_stack(arena, offs)
+    decided_long = 0
+    for i in range(len(reqs)):
+        if used[i] <= ENVOY_THREAD_STACK:
+            assert got[i] == exp[i], (i, int(got[i]), int(exp[i]), int(used[i]))
+        elif got[i] != L.VERDICT_UNSUPPORTED:
+            assert got[i] == exp[i], (i, int(got[i]), int(exp[i]), int(used[i]))
+            decided_long += 1
+        if got[i] == L.VERDICT_UNSUPPORTED:
+            assert used[i] > ENVOY_THREAD_STACK, (i, int(used[i]))
+    assert got[:6].tolist() == [0] * 6  # n = 8 k, 12 k, 20 k decided (round 4: -3 from 12 k)
+    assert decided_long > 0 and L.VERDICT_UNSUPPORTED in got.tolist()
+    assert got.tolist() == HttpProgram(rs.program()).eval(arena, offs).tolist()
+
+
+def test_extended_rules_slow_pass_share(gpu):
+    """bench.py --extended's workload: config 2 with the extended rules in
+    front.  Most requests are deferred to the slow pass (the back-reference
+    rule's superset automaton matches config-2 paths); no verdict is −3."""
+    rules = list(X.REALISTIC) + W.rules(2)
+    arena, offs = W.requests(2, 5_000_000, 300_000, n_rules=1000)
+    got = _check(rules, arena, offs)
+    assert L.VERDICT_UNSUPPORTED not in got.tolist()
