@@ -174,6 +174,69 @@ int build_search_groups(const std::vector<const re::Ast*>& asts, std::vector<uin
   return build_search_groups(asts, std::move(b), out, err);
 }
 
+// RE2-dialect gram filter of one field (program.h FieldDesc::gram_tab): a
+// 2-entry-bucket table 4-byte gram -> mask of search groups (bit j % 32 of
+// the field's search group j).  Each pattern with a required literal is
+// entered under ONE of its literal's grams -- the rarest among the field's
+// patterns whose bucket has room --, so a value that contains none of a
+// group's chosen grams cannot match any of the group's patterns and the
+// group's automaton is not walked.
+struct GramFilter {
+  bool on = false;
+  uint32_t search_first = 0;  // field group index of the first search group
+  uint32_t always = 0;        // groups walked for every value
+  std::vector<uint32_t> tab;  // buckets x {gram, mask, gram, mask}
+};
+
+void build_gram_filter(const std::vector<Group>& groups, uint32_t first, uint32_t first_lit,
+                       const std::vector<std::vector<uint32_t>>& grams, GramFilter* out) {
+  const uint32_t ns = static_cast<uint32_t>(groups.size()) - first;
+  out->search_first = first;
+  if (ns < kGramMinGroups || ns > kGramMaxGroups || first_lit == groups.size()) return;
+  std::map<uint32_t, uint32_t> freq;
+  uint32_t n_lit = 0;
+  for (uint32_t j = first_lit; j < groups.size(); ++j)
+    for (uint32_t p : groups[j].pats) {
+      for (uint32_t g : grams[p]) ++freq[g];
+      ++n_lit;
+    }
+  uint32_t buckets = 64;
+  while (buckets < n_lit) buckets <<= 1;
+  if (buckets > 65536) return;
+  out->tab.assign(4ull * buckets, 0u);
+  for (uint32_t j = first; j < first_lit; ++j) out->always |= 1u << ((j - first) & 31u);
+  for (uint32_t j = first_lit; j < groups.size(); ++j) {
+    const uint32_t bit = 1u << ((j - first) & 31u);
+    for (uint32_t p : groups[j].pats) {
+      uint32_t best = kNone, best_freq = kNone;
+      int best_slot = -1;
+      for (uint32_t g : grams[p]) {
+        uint32_t* b = &out->tab[4ull * (gram_bucket(g) & (buckets - 1))];
+        int slot = -1;
+        for (int e = 0; e < 2 && slot < 0; ++e)
+          if (b[2 * e + 1] && b[2 * e] == g) slot = e;  // already entered: shares the entry
+        for (int e = 0; e < 2 && slot < 0; ++e)
+          if (!b[2 * e + 1]) slot = e;
+        if (slot < 0) continue;
+        const uint32_t fq = freq[g];
+        if (fq < best_freq) {
+          best = g;
+          best_freq = fq;
+          best_slot = slot;
+        }
+      }
+      if (best_slot < 0) {  // every bucket of its grams is full: walk the group always
+        out->always |= bit;
+        continue;
+      }
+      uint32_t* b = &out->tab[4ull * (gram_bucket(best) & (buckets - 1))];
+      b[2 * best_slot] = best;
+      b[2 * best_slot + 1] |= bit;
+    }
+  }
+  out->on = true;
+}
+
 // Build the field automata of one field's patterns: normally ONE automaton
 // (dfa_pack.h, linear in the rules for prefix-diverging sets); a set whose
 // product exceeds the limits (e.g. unanchored RE2-search patterns, which never
@@ -332,6 +395,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   std::vector<std::vector<std::vector<uint32_t>>> slow_vm(nf);
   // field pattern -> (group, local id)
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fp_loc(nf);
+  std::vector<GramFilter> gram(nf);  // RE2 dialect: per field, which search groups a value may need
   for (uint32_t f = 0; f < nf; ++f) {
     if (fpats[f].empty()) continue;
     std::vector<re::Ast> asts(fpats[f].size());
@@ -400,8 +464,32 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
     }
     if (!sidx.empty()) {
-      int rc = build_search_groups(ptrs, sidx, &groups[f], &err);
-      if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+      // patterns without a 4-byte required literal ("always" walked) are
+      // grouped apart from the others, so the gram filter can skip whole groups
+      std::vector<std::vector<uint32_t>> grams(fpats[f].size());
+      std::vector<uint32_t> s_always, s_lit;
+      for (uint32_t p : sidx) {
+        for (const std::string& lit : re::required_literals(asts[p]))
+          for (size_t i = 0; i + 4 <= lit.size(); ++i) {
+            uint32_t g;
+            std::memcpy(&g, lit.data() + i, 4);
+            grams[p].push_back(g);
+          }
+        std::sort(grams[p].begin(), grams[p].end());
+        grams[p].erase(std::unique(grams[p].begin(), grams[p].end()), grams[p].end());
+        (grams[p].empty() ? s_always : s_lit).push_back(p);
+      }
+      const uint32_t first = static_cast<uint32_t>(groups[f].size());
+      if (!s_always.empty()) {
+        int rc = build_search_groups(ptrs, s_always, &groups[f], &err);
+        if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+      }
+      const uint32_t first_lit = static_cast<uint32_t>(groups[f].size());
+      if (!s_lit.empty()) {
+        int rc = build_search_groups(ptrs, s_lit, &groups[f], &err);
+        if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+      }
+      build_gram_filter(groups[f], first, first_lit, grams, &gram[f]);
     }
     fp_loc[f].assign(fpats[f].size(), {0, 0});
     for (uint32_t g = 0; g < groups[f].size(); ++g)
@@ -616,6 +704,10 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     fd[f].dfa_first = dfa_first[f];
     fd[f].ndfa = static_cast<uint32_t>(groups[f].size());
     fd[f].presence = push_records(pres_keyed[f]);
+    fd[f].gram_tab = kNone;  // placed in the LDS image below
+    fd[f].gram_mask = 0;
+    fd[f].always = ~0u;
+    fd[f].search_first = gram[f].search_first;
   }
   std::vector<Span> rremote(n);
   for (size_t i = 0; i < n; ++i) rremote[i] = push_list(remotes[i]);
@@ -673,6 +765,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       lds_name_tab = img_take(4ull * name_slots);
       for (uint32_t f = 3; f < nf; ++f) name_off.push_back(img_take((field_names[f].size() + 3) / 4));
     }
+  }
+  // RE2-dialect gram filters (read once per value byte): right after the name table
+  for (uint32_t f = 0; f < nf; ++f) {
+    if (!gram[f].on || img + gram[f].tab.size() > budget) continue;
+    fd[f].gram_tab = img_take(gram[f].tab.size());
+    fd[f].gram_mask = static_cast<uint32_t>(gram[f].tab.size() / 4 - 1);
+    fd[f].always = gram[f].always;
   }
   // (policy, direction, port) -> port entry table (open addressing on
   // ent_hash, program.h); in LDS when small
@@ -940,6 +1039,8 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   }
   std::memcpy(P + h.off_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
   std::memcpy(I + lds_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
+  for (uint32_t f = 0; f < nf; ++f)
+    if (fd[f].gram_tab != kNone) std::memcpy(I + fd[f].gram_tab, gram[f].tab.data(), gram[f].tab.size() * 4ull);
   std::memcpy(P + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));
   std::memcpy(I + lds_fields, fd.data(), fd.size() * sizeof(FieldDesc));
   if (lds_name_tab != kNone) {

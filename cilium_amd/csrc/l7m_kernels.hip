@@ -424,17 +424,26 @@ struct Codes<0> {
 // value DFA, dozens of DFAs, kept in a global scratch column per thread
 // (stride = the grid's threads); agent-scope loads and stores, so a later
 // tile never reads a stale line of an earlier one.
+// With <= 64 value DFAs a per-lane mask of the DFAs this record walked
+// stands in for clearing the column (the gram filter leaves most unwalked).
 template <>
 struct Codes<-1> {
   uint32_t* p;
   uint32_t stride;
+  uint64_t valid;
+  bool masked;
   __device__ __forceinline__ void clear(uint32_t n) {
-    for (uint32_t d = 0; d < n; ++d) __hip_atomic_store(p + d * stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    valid = 0;
+    masked = n <= 64;
+    if (!masked)
+      for (uint32_t d = 0; d < n; ++d) __hip_atomic_store(p + d * stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __device__ __forceinline__ void set(uint32_t d, uint32_t v) {
     __hip_atomic_store(p + d * stride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    valid |= d < 64 ? 1ull << d : 0ull;
   }
   __device__ __forceinline__ uint32_t get(uint32_t d) const {
+    if (masked && !((valid >> d) & 1ull)) return 0u;
     uint32_t v = __hip_atomic_load(p + d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" : "+v"(v));
     return v;
@@ -509,6 +518,71 @@ __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j)
     out[j] = j < m ? acc[j] | gld(c.prog + c.dds[d0 + j].es_off + st[j]) : 0u;
+}
+
+// The same with a per-lane DFA per chain (the gram filter's selection):
+// chain j walks DFA d[j] when j < m (m per lane).
+template <class Src>
+__device__ __forceinline__ void walk_search4v(const Ctx& c, const uint32_t (&d)[4], uint32_t m, const Src& src,
+                                              uint32_t pos, uint32_t len, uint32_t (&out)[4]) {
+  const uint32_t* T[4];
+  const uint8_t* cm[4];
+  const uint32_t* mid[4];
+  uint32_t ncls[4], st[4], acc[4], cml[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const DfaDesc& dd = c.dds[d[j < m ? j : 0u]];
+    T[j] = c.prog + dd.table_off;
+    cm[j] = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
+    cml[j] = dd.lds_table != kNone ? 4u * dd.lds_table : kNone;
+    mid[j] = c.prog + dd.acc_mid_off;
+    ncls[j] = dd.acc_ncls;
+    st[j] = dd.start_base;
+    acc[j] = dd.start_es8;
+  }
+  for (uint32_t k = 0; k < len; ++k) {
+    const uint32_t b = src.byte(pos + k);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      if (j < m) {
+        const uint32_t e = gld(T[j] + st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b));
+        st[j] = e & 0xffffffu;
+        acc[j] |= gld(mid[j] + (e >> 24));
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) out[j] = j < m ? acc[j] | gld(c.prog + c.dds[d[j]].es_off + st[j]) : 0u;
+}
+
+// RE2-dialect gram filter (program.h FieldDesc::gram_tab): bit j % 32 of the
+// result = the field's search group j may match.  Every 4-byte window of the
+// value is one independent probe of a 2-entry LDS bucket (no dependent chain).
+template <class Src>
+__device__ __forceinline__ uint32_t gram_select(const Ctx& c, const FieldDesc& fd, const Src& src, uint32_t pos,
+                                                uint32_t len) {
+  uint32_t m = fd.always;
+  if (len < 4) return m;
+  const u32x4* tab = reinterpret_cast<const u32x4*>(c.img + fd.gram_tab);
+  const uint32_t gm = fd.gram_mask, end = pos + len - 3;  // grams start in [pos, end)
+  auto probe = [&](uint32_t g, bool on) {
+    const u32x4 e = tab[on ? gram_bucket(g) & gm : 0u];
+    m |= on ? ((e.x == g ? e.y : 0u) | (e.z == g ? e.w : 0u)) : 0u;
+  };
+  if constexpr (Src::kLds) {
+    uint32_t q = pos & ~3u;
+    uint32_t w0 = src.word(q >> 2);
+    for (; q < end; q += 4) {
+      const uint32_t w1 = src.word((q >> 2) + 1);
+#pragma unroll
+      for (uint32_t sft = 0; sft < 4; ++sft)
+        probe(__builtin_amdgcn_alignbyte(w1, w0, sft), q + sft >= pos && q + sft < end);
+      w0 = w1;
+    }
+  } else {
+    for (uint32_t q = pos; q < end; ++q) probe(src.word_u(q), true);
+  }
+  return m;
 }
 
 template <bool kLit, bool kSearch, class Src>
@@ -775,7 +849,32 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
     if (f != kNone) {
       present |= 1ull << f;
       const FieldDesc& fd = c.fields[f];
-      for (uint32_t k = 0; k < fd.ndfa; ++k) {
+      uint32_t kend = fd.ndfa;
+      if constexpr (kReg < 0) {
+        if (fd.gram_tab != kNone) {
+          // the search groups the value's grams select, up to four chains at a
+          // time (per lane: its own groups); the packed groups before them below
+          const uint32_t sel = gram_select(c, fd, src, p, len), ns = fd.ndfa - fd.search_first;
+          uint64_t selm = ns > 32 ? (static_cast<uint64_t>(sel) << 32 | sel) : sel;
+          if (ns < 64) selm &= (1ull << ns) - 1;
+          while (__any(selm != 0)) {
+            uint32_t dl[4], m = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+              dl[j] = fd.dfa_first + fd.search_first + (selm ? static_cast<uint32_t>(__builtin_ctzll(selm)) : 0u);
+              m = selm ? j + 1 : m;
+              selm &= selm - 1;
+            }
+            uint32_t out[4];
+            walk_search4v(c, dl, m, src, p, len, out);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+              if (j < m) codes.set(dl[j], out[j]);
+          }
+          kend = fd.search_first;
+        }
+      }
+      for (uint32_t k = 0; k < kend; ++k) {
         const uint32_t d = fd.dfa_first + k;
         if constexpr (kReg < 0) {
           if (c.dds[d].kind == kDfaSearch) {  // a run of search automata, four at a time

@@ -151,7 +151,21 @@ constexpr uint32_t kMaxLdsCtmaskWords = 256;     // candidate-presence bitmask k
 struct FieldDesc {
   uint32_t dfa_first, ndfa;  // value DFAs of this field (contiguous)
   Span presence;             // check-record list keyed on "field present"
+  // RE2-dialect gram filter (kReg = -1 programs): the field's search groups
+  // are DFAs [dfa_first + search_first, dfa_first + ndfa); group j is walked
+  // only when bit j % 32 of (always | the masks of the 4-byte grams the value
+  // contains) is set.  gram_tab: LDS image word offset of gram_mask + 1
+  // buckets of {gram, mask, gram, mask} (mask 0 = empty entry), bucket =
+  // gram_bucket(gram) & gram_mask; kNone = no filter (walk every group).
+  uint32_t gram_tab, gram_mask, always, search_first;
 };
+static_assert(sizeof(FieldDesc) == 32, "field desc is 8 words");
+// Every match of a pattern contains its required literal (regex_re2.cc
+// required_literals), so a value lacking all of a group's chosen 4-byte grams
+// cannot match any of the group's patterns.
+constexpr uint32_t kGramMinGroups = 3;      // fields with fewer search groups walk them all
+constexpr uint32_t kGramMaxGroups = 64;
+__host__ __device__ inline uint32_t gram_bucket(uint32_t gram) { return (gram * 0x9e3779b1u) >> 16; }
 
 // Check record (u32 words, in the check-record pool; lists are sorted by rid):
 //   [0] rule id   [1] n_matchers | port entry << 8 | (has_remote_set << 31)

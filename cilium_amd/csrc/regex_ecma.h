@@ -108,6 +108,10 @@ void make_search_prefix(Ast* a);
 // under regexp.MatchString, regex_re2.cc).
 void simplify_search(Ast* a);
 
+// Byte strings every match of the pattern contains (regex_re2.cc): the
+// literal runs of its top-level structure.  Empty when nothing is required.
+std::vector<std::string> required_literals(const Ast& a);
+
 }  // namespace re
 
 // The slow path's program for a full AST (regex_vm.cc, executed by

@@ -497,6 +497,91 @@ void simplify_search(Ast* a) {
   a->root = static_cast<int>(a->nodes.size()) - 1;
 }
 
+// Required literals: the maximal byte strings every match of the pattern
+// contains (runs of single-byte atoms in a concatenation, a repeated exact
+// atom's minimum, the exact string of a fully literal subexpression).
+// Alternations and optional parts contribute nothing: the result is a set of
+// necessary substrings, never a sufficient one.
+namespace {
+struct LitInfo {
+  bool exact = false;          // the node matches exactly this one string
+  std::string str;             // ... it
+  std::vector<std::string> req;  // required substrings (non-exact nodes)
+};
+LitInfo lit_info(const Ast& a, int id, int depth) {
+  const Node& n = a.nodes[id];
+  LitInfo r;
+  if (depth > 200) return r;  // deep nesting: nothing required (still a superset)
+  switch (n.kind) {
+    case Node::Empty:
+    case Node::Bol:
+    case Node::Eol:
+    case Node::WordB:
+    case Node::Look:
+      r.exact = true;  // zero-width
+      return r;
+    case Node::Set:
+      if (n.set.count() == 1) {
+        for (int b = 0; b < 256; ++b)
+          if (n.set.test(b)) r.str.push_back(static_cast<char>(b));
+        r.exact = true;
+      }
+      return r;
+    case Node::Group:
+      return lit_info(a, n.kids[0], depth + 1);
+    case Node::Cat: {
+      std::string run;
+      r.exact = true;
+      for (int k : n.kids) {
+        LitInfo c = lit_info(a, k, depth + 1);
+        if (c.exact) {
+          run += c.str;
+          continue;
+        }
+        r.exact = false;
+        if (!run.empty()) r.req.push_back(run);
+        run.clear();
+        for (auto& s : c.req) r.req.push_back(std::move(s));
+      }
+      if (r.exact) {
+        r.str = run;
+      } else if (!run.empty()) {
+        r.req.push_back(run);
+      }
+      return r;
+    }
+    case Node::Rep: {
+      LitInfo c = lit_info(a, n.kids[0], depth + 1);
+      if (n.min == 0) return r;
+      if (c.exact) {
+        std::string s;
+        for (int i = 0; i < n.min && s.size() < 64; ++i) s += c.str;
+        if (n.max == n.min && s.size() < 64) {
+          r.exact = true;
+          r.str = s;
+        } else if (!s.empty()) {
+          r.req.push_back(s);
+        }
+        return r;
+      }
+      r.req = std::move(c.req);
+      return r;
+    }
+    default:  // Alt, Backref: no required substring
+      return r;
+  }
+}
+}  // namespace
+
+std::vector<std::string> required_literals(const Ast& a) {
+  LitInfo r = lit_info(a, a.root, 0);
+  if (r.exact) return r.str.empty() ? std::vector<std::string>{} : std::vector<std::string>{r.str};
+  std::vector<std::string> out;
+  for (auto& s : r.req)
+    if (!s.empty()) out.push_back(std::move(s));
+  return out;
+}
+
 void make_search(Ast* a) {
   Node any;
   any.kind = Node::Set;

@@ -75,8 +75,28 @@ class HttpProgram:
             g = h["off_dfas"] + DFA_WORDS * k
             assert self.w[g:g + DFA_WORDS] == self.img[o:o + DFA_WORDS]
             self.dfas.append(d)
-        self.fields = [tuple(self.img[h["lds_fields"] + 4 * f: h["lds_fields"] + 4 * f + 4])
+        # program.h FieldDesc (8 words): dfa_first, ndfa, presence off/len,
+        # gram_tab, gram_mask, always, search_first
+        self.fields = [tuple(self.img[h["lds_fields"] + 8 * f: h["lds_fields"] + 8 * f + 8])
                        for f in range(h["n_fields"])]
+
+    def gram_select(self, f, data: bytes):
+        """RE2-dialect gram filter (program.h FieldDesc::gram_tab): the mask
+        of search groups (bit j % 32) a value must walk; None = walk all."""
+        fd = self.fields[f]
+        tab, gmask, always = fd[4], fd[5], fd[6]
+        if tab == KNONE:
+            return None
+        m = always
+        for i in range(len(data) - 3):
+            g = int.from_bytes(data[i:i + 4], "little")
+            b = tab + 4 * ((((g * 0x9E3779B1) & 0xFFFFFFFF) >> 16) & gmask)
+            e = self.img[b:b + 4]
+            if e[0] == g:
+                m |= e[1]
+            if e[2] == g:
+                m |= e[3]
+        return m
 
     def name_tab_lookup(self, name: bytes):
         h = self.h
@@ -277,8 +297,13 @@ class HttpProgram:
 
         def eval_field(f, data):
             fvals[f] = data
-            first, nd, _po, _pl = self.fields[f]
+            first, nd = self.fields[f][0], self.fields[f][1]
+            sf = self.fields[f][7]
+            sel = self.gram_select(f, data)
             for k in range(first, first + nd):
+                if sel is not None and k - first >= sf and not (sel >> ((k - first - sf) & 31)) & 1:
+                    codes[k] = 0  # no chosen gram of the group's patterns: not walked
+                    continue
                 codes[k] = self.walk(k, data)
 
         for f, flag, ln in ((0, L.F_METHOD, mlen), (1, L.F_PATH, plen), (2, L.F_AUTHORITY, alen)):

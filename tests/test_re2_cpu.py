@@ -117,3 +117,54 @@ def test_search_trailing_repetition_cut_is_exact():
         subs = [s.encode() for s in subjects]
         got = _interp_paths(pattern, subs)
         assert [int(v) == 0 for v in got] == [bool(regex_search(pattern, s)) for s in subs], pattern
+
+
+def _gram_rules(rng, n):
+    """Random RE2 path patterns, most with required literals (the gram filter's
+    input) in every structural position: prefix, middle, repeated, inside
+    groups, behind optional parts; some with none (always-walked groups)."""
+    words = ["alpha", "bravo", "char", "delt", "echo1", "fox/", "/gol", "hot-", "ind.", "jul_"]
+    out = []
+    for i in range(n):
+        w = str(rng.choice(words)) + str(i % 37)
+        form = int(rng.integers(0, 9))
+        p = ["/%s/v[0-9]+" % w, "[a-z]*%s(x|y)?" % w, "(%s)+z" % w, "^/(api|svc)/%s" % w, "%s{2}" % w,
+             "q?%s[^/]*/" % w, "(ab|cd)[0-9]", "[a-c]{2,3}d", "%s$" % w][form]
+        out.append(L.PortRuleHTTP(Path=p, Method=str(rng.choice(["", "GET", "(PUT|POST)"]))))
+    return out
+
+
+def _gram_subjects(rng, rules, n):
+    """Paths that contain some rule's literal (hits and near misses)."""
+    subs = []
+    for _ in range(n):
+        r = rules[int(rng.integers(0, len(rules)))].Path
+        lit = "".join(ch for ch in r if ch.isalnum() or ch in "/-._")
+        cut = int(rng.integers(0, len(lit) + 1))
+        s = str(rng.choice(["", "/", "/api/", "/svc/", "xx"])) + lit[:cut] + str(rng.choice(["", "7", "z", "/", "v12/"]))
+        if rng.random() < 0.3:
+            s = s + s
+        subs.append(s)
+    return subs
+
+
+def test_gram_filter_is_exact_on_random_literal_patterns():
+    """program.h FieldDesc::gram_tab: with >= 3 search groups on :path the
+    filter skips groups whose chosen grams a value lacks; the interpreter
+    (walking only the selected groups, as the kernel does) equals the oracle,
+    and the filter actually skips most groups."""
+    rng = np.random.default_rng(33)
+    for trial in range(3):
+        rules = _gram_rules(rng, 200 + 100 * trial)
+        prog = HttpProgram(L.RuleSet.compile_http(rules, dialect=RE2).program())
+        fd = prog.fields[1]
+        assert fd[4] != 0xFFFFFFFF, "path field without a gram filter"
+        reqs = [L.HTTPRequest(str(rng.choice(["GET", "PUT", "POST"])), s) for s in _gram_subjects(rng, rules, 1500)]
+        arena, offs = L.pack_http(reqs)
+        got = prog.eval(arena, offs)
+        exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
+        bad = np.nonzero(got != exp)[0]
+        assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
+        assert (exp >= 0).sum() > 100
+        walked = [bin(prog.gram_select(1, r.path.encode())).count("1") for r in reqs[:300]]
+        assert np.mean(walked) < 0.5 * (fd[1] - fd[7])

@@ -63,12 +63,14 @@ def test_slow_path_decides_what_the_reference_decides(gpu):
     8 MiB thread stack (an Envoy worker's) gets the reference's verdict; −3
     appears only where the oracle measured more than 8 MiB of native stack,
     i.e. where std::regex_match would overflow the worker and crash Envoy."""
-    rules = [L.PortRuleHTTP(Path="/(a)(?:.)*\\1z"), L.PortRuleHTTP(Path="/(a)(b|c)*\\1z"),
+    # rule 0 (4 executor words per byte) decides the b-runs; the c-runs reach
+    # rule 1 (16 words per byte, 834 native bytes per byte in libstdc++)
+    rules = [L.PortRuleHTTP(Path="/(a)(?:b)*\\1z"), L.PortRuleHTTP(Path="/(a)(b|c)*\\1z"),
              L.PortRuleHTTP(Path="/.*")]
     sizes = (10, 100, 2000, 8000, 12000, 20000, 40000, 60000)
     reqs = [L.HTTPRequest("GET", "/a" + "b" * n + "az") for n in sizes]
-    reqs += [L.HTTPRequest("GET", "/a" + "b" * n + "ay") for n in sizes]  # rule 2 decides after two failures
-    reqs += [L.HTTPRequest("GET", "/a" + "c" * n + "az") for n in (5000, 20000)]
+    reqs += [L.HTTPRequest("GET", "/a" + "b" * n + "ay") for n in sizes]  # rule 2 decides
+    reqs += [L.HTTPRequest("GET", "/a" + "c" * n + "az") for n in (2000, 8000, 12000, 20000, 40000)]
     arena, offs = L.pack_http(reqs)
     rs = L.RuleSet.compile_http(rules)
     got = rs.eval(arena, offs)
