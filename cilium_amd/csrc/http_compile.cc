@@ -480,16 +480,22 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
         (grams[p].empty() ? s_always : s_lit).push_back(p);
       }
       const uint32_t first = static_cast<uint32_t>(groups[f].size());
-      if (!s_always.empty()) {
-        int rc = build_search_groups(ptrs, s_always, &groups[f], &err);
+      if (sidx.size() <= kSearchMaxPats) {  // one group: walked anyway, no filter
+        int rc = build_search_groups(ptrs, sidx, &groups[f], &err);
         if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+        gram[f].search_first = first;
+      } else {
+        if (!s_always.empty()) {
+          int rc = build_search_groups(ptrs, s_always, &groups[f], &err);
+          if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+        }
+        const uint32_t first_lit = static_cast<uint32_t>(groups[f].size());
+        if (!s_lit.empty()) {
+          int rc = build_search_groups(ptrs, s_lit, &groups[f], &err);
+          if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
+        }
+        build_gram_filter(groups[f], first, first_lit, grams, &gram[f]);
       }
-      const uint32_t first_lit = static_cast<uint32_t>(groups[f].size());
-      if (!s_lit.empty()) {
-        int rc = build_search_groups(ptrs, s_lit, &groups[f], &err);
-        if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
-      }
-      build_gram_filter(groups[f], first, first_lit, grams, &gram[f]);
     }
     fp_loc[f].assign(fpats[f].size(), {0, 0});
     for (uint32_t g = 0; g < groups[f].size(); ++g)
@@ -663,6 +669,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     dd[k].lds_skip = kNone;
     dd[k].skip_lim = 0;
     dd[k].kind = kDfaPacked;
+    dd[k].lds_search = dd[k].lds_mid = kNone;
     if (all[k].grp && all[k].grp->search) {
       const SearchDfa& sd = all[k].grp->sd;
       dd[k].kind = kDfaSearch;
@@ -773,6 +780,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     fd[f].gram_mask = static_cast<uint32_t>(gram[f].tab.size() / 4 - 1);
     fd[f].always = gram[f].always;
   }
+  // search automata's mid masks (one read per value byte, <= 256 words each):
+  // in LDS, so a search step costs one L2 request (the table entry), not two
+  for (uint32_t k = 0; k < ndt; ++k) {
+    if (!all[k].grp || !all[k].grp->search) continue;
+    const uint64_t mw = all[k].grp->sd.midmask.size();
+    if (img + ((mw + 3) & ~3ull) <= budget) dd[k].lds_mid = img_take(mw);
+  }
   // (policy, direction, port) -> port entry table (open addressing on
   // ent_hash, program.h); in LDS when small
   uint32_t ent_slots = 2;
@@ -806,6 +820,12 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   for (uint32_t k : order) {
     if (dd[k].kind == kDfaSearch) {  // walked from the program; the 256-byte class map in LDS when it fits
       if (img + 64 <= budget) dd[k].lds_table = img_take(64);
+      // small automata (a method's, a few hosts'): the dense table and its mid
+      // masks too, so their steps read LDS instead of L2
+      const SearchDfa& sd = all[k].grp->sd;
+      const uint64_t tw = sd.table.size();
+      if (dd[k].lds_table != kNone && dd[k].lds_mid != kNone && tw <= kLdsSearchMaxWords && img + tw <= budget)
+        dd[k].lds_search = img_take(tw);
       continue;
     }
     const PackedDfa& d = *all[k].d;
@@ -984,6 +1004,8 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       std::memcpy(P + dd[k].es_off, sd.endmask.data(), sd.endmask.size() * 4ull);
       std::memcpy(P + dd[k].acc_cmap_off, sd.cmap, 256);
       if (dd[k].lds_table != kNone) std::memcpy(I + dd[k].lds_table, sd.cmap, 256);
+      if (dd[k].lds_search != kNone) std::memcpy(I + dd[k].lds_search, sd.table.data(), sd.table.size() * 4ull);
+      if (dd[k].lds_mid != kNone) std::memcpy(I + dd[k].lds_mid, sd.midmask.data(), sd.midmask.size() * 4ull);
       std::memcpy(P + dd[k].acc_mid_off, sd.midmask.data(), sd.midmask.size() * 4ull);
     } else {
       std::memcpy(P + dd[k].table_off, d.table.data(), d.n_slots * 4ull);

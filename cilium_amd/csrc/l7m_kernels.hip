@@ -424,26 +424,54 @@ struct Codes<0> {
 // value DFA, dozens of DFAs, kept in a global scratch column per thread
 // (stride = the grid's threads); agent-scope loads and stores, so a later
 // tile never reads a stale line of an earlier one.
-// With <= 64 value DFAs a per-lane mask of the DFAs this record walked
-// stands in for clearing the column (the gram filter leaves most unwalked).
+// Search programs' end codes: the first kSearchRegCodes DFAs a record walks
+// keep their codes in registers (the gram filter leaves a handful walked per
+// record); more spill to a global scratch column per thread (stride = the
+// grid's threads).  With <= 64 value DFAs a per-lane mask of the walked DFAs
+// stands in for clearing the column.  (Round 4 kept every code in the
+// column: config 2 RE2 spent ~40 % of a tile in verification on those L2
+// round trips and the column evicted the search tables from L2.)
+constexpr uint32_t kSearchRegCodes = 4;
 template <>
 struct Codes<-1> {
   uint32_t* p;
   uint32_t stride;
   uint64_t valid;
   bool masked;
+  uint32_t nr;
+  uint32_t rd[kSearchRegCodes], rv[kSearchRegCodes];
   __device__ __forceinline__ void clear(uint32_t n) {
     valid = 0;
     masked = n <= 64;
+    nr = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSearchRegCodes; ++i) rd[i] = kNone;
     if (!masked)
       for (uint32_t d = 0; d < n; ++d) __hip_atomic_store(p + d * stride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __device__ __forceinline__ void set(uint32_t d, uint32_t v) {
-    __hip_atomic_store(p + d * stride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (nr < kSearchRegCodes) {
+#pragma unroll
+      for (uint32_t i = 0; i < kSearchRegCodes; ++i) {
+        rd[i] = nr == i ? d : rd[i];
+        rv[i] = nr == i ? v : rv[i];
+      }
+      ++nr;
+    } else {
+      __hip_atomic_store(p + d * stride, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     valid |= d < 64 ? 1ull << d : 0ull;
   }
   __device__ __forceinline__ uint32_t get(uint32_t d) const {
     if (masked && !((valid >> d) & 1ull)) return 0u;
+    uint32_t r = 0;
+    bool f = false;
+#pragma unroll
+    for (uint32_t i = 0; i < kSearchRegCodes; ++i) {
+      r = rd[i] == d ? rv[i] : r;
+      f |= rd[i] == d;
+    }
+    if (f) return r;
     uint32_t v = __hip_atomic_load(p + d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" : "+v"(v));
     return v;
@@ -474,10 +502,22 @@ __device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd,
   const uint32_t* __restrict__ mid = c.prog + dd.acc_mid_off;
   const uint32_t ncls = dd.acc_ncls;
   uint32_t st = dd.start_base, acc = dd.start_es8;
+  if (dd.lds_search != kNone) {  // small automaton: table and mid masks in LDS
+    const uint32_t* LT = c.img + dd.lds_search;
+    const uint32_t* LM = c.img + dd.lds_mid;
+    for (uint32_t k = 0; k < len; ++k) {
+      const uint32_t e = lld(LT + st * ncls + cmap_byte(cml, cm, src.byte(pos + k)));
+      st = e & 0xffffffu;
+      acc |= lld(LM + (e >> 24));
+    }
+    return acc | gld(c.prog + dd.es_off + st);
+  }
+  // mid masks in LDS when placed there (generic pointer: one flat read)
+  const uint32_t* M = dd.lds_mid != kNone ? c.img + dd.lds_mid : mid;
   for (uint32_t k = 0; k < len; ++k) {
     const uint32_t e = gld(T + st * ncls + cmap_byte(cml, cm, src.byte(pos + k)));
     st = e & 0xffffffu;
-    acc |= gld(mid + (e >> 24));
+    acc |= M[e >> 24];
   }
   return acc | gld(c.prog + dd.es_off + st);
 }
@@ -486,32 +526,37 @@ __device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd,
 // field) over the same bytes, interleaved: their table reads are independent,
 // so m L2 round trips are in flight per byte instead of one (config 2 in the
 // RE2 dialect walks ~32 automata per path).
-template <class Src>
+// kL: every chain's table is in LDS (lds_search); else all are read from the
+// program (LDS-resident tables have their program copy too).
+template <bool kL, class Src>
 __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t m, const Src& src, uint32_t pos,
                                              uint32_t len, uint32_t (&out)[4]) {
   const uint32_t* T[4];
   const uint8_t* cm[4];
   const uint32_t* mid[4];
-  uint32_t ncls[4], st[4], acc[4], cml[4];
+  uint32_t ncls[4], st[4], acc[4], cml[4], lt[4], lm[4];
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
     const DfaDesc& dd = c.dds[d0 + (j < m ? j : 0u)];
     T[j] = c.prog + dd.table_off;
     cm[j] = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
     cml[j] = dd.lds_table != kNone ? 4u * dd.lds_table : kNone;
-    mid[j] = c.prog + dd.acc_mid_off;
+    mid[j] = dd.lds_mid != kNone ? c.img + dd.lds_mid : c.prog + dd.acc_mid_off;  // generic: LDS or program
     ncls[j] = dd.acc_ncls;
     st[j] = dd.start_base;
     acc[j] = dd.start_es8;
+    lt[j] = dd.lds_search;  // kNone: table in the program (L2)
+    lm[j] = dd.lds_mid;
   }
   for (uint32_t k = 0; k < len; ++k) {
     const uint32_t b = src.byte(pos + k);
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
       if (j < m) {
-        const uint32_t e = gld(T[j] + st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b));
+        const uint32_t ci = st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b);
+        const uint32_t e = kL ? lld(c.img + lt[j] + ci) : gld(T[j] + ci);
         st[j] = e & 0xffffffu;
-        acc[j] |= gld(mid[j] + (e >> 24));
+        acc[j] |= kL ? lld(c.img + lm[j] + (e >> 24)) : mid[j][e >> 24];
       }
     }
   }
@@ -522,32 +567,35 @@ __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t
 
 // The same with a per-lane DFA per chain (the gram filter's selection):
 // chain j walks DFA d[j] when j < m (m per lane).
-template <class Src>
+template <bool kL, class Src>
 __device__ __forceinline__ void walk_search4v(const Ctx& c, const uint32_t (&d)[4], uint32_t m, const Src& src,
                                               uint32_t pos, uint32_t len, uint32_t (&out)[4]) {
   const uint32_t* T[4];
   const uint8_t* cm[4];
   const uint32_t* mid[4];
-  uint32_t ncls[4], st[4], acc[4], cml[4];
+  uint32_t ncls[4], st[4], acc[4], cml[4], lt[4], lm[4];
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
     const DfaDesc& dd = c.dds[d[j < m ? j : 0u]];
     T[j] = c.prog + dd.table_off;
     cm[j] = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
     cml[j] = dd.lds_table != kNone ? 4u * dd.lds_table : kNone;
-    mid[j] = c.prog + dd.acc_mid_off;
+    mid[j] = dd.lds_mid != kNone ? c.img + dd.lds_mid : c.prog + dd.acc_mid_off;  // generic: LDS or program
     ncls[j] = dd.acc_ncls;
     st[j] = dd.start_base;
     acc[j] = dd.start_es8;
+    lt[j] = dd.lds_search;  // kNone: table in the program (L2)
+    lm[j] = dd.lds_mid;
   }
   for (uint32_t k = 0; k < len; ++k) {
     const uint32_t b = src.byte(pos + k);
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
       if (j < m) {
-        const uint32_t e = gld(T[j] + st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b));
+        const uint32_t ci = st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b);
+        const uint32_t e = kL ? lld(c.img + lt[j] + ci) : gld(T[j] + ci);
         st[j] = e & 0xffffffu;
-        acc[j] |= gld(mid[j] + (e >> 24));
+        acc[j] |= kL ? lld(c.img + lm[j] + (e >> 24)) : mid[j][e >> 24];
       }
     }
   }
@@ -855,6 +903,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
           // the search groups the value's grams select, up to four chains at a
           // time (per lane: its own groups); the packed groups before them below
           const uint32_t sel = gram_select(c, fd, src, p, len), ns = fd.ndfa - fd.search_first;
+          HPROF(6);  // (diagnostic build) the gram filter
           uint64_t selm = ns > 32 ? (static_cast<uint64_t>(sel) << 32 | sel) : sel;
           if (ns < 64) selm &= (1ull << ns) - 1;
           while (__any(selm != 0)) {
@@ -866,22 +915,25 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
               selm &= selm - 1;
             }
             uint32_t out[4];
-            walk_search4v(c, dl, m, src, p, len, out);
+            walk_search4v<false>(c, dl, m, src, p, len, out);  // (LDS-resident tables keep a program copy)
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
               if (j < m) codes.set(dl[j], out[j]);
           }
+          HPROF(3);  // gram filter + the selected groups' walks
           kend = fd.search_first;
         }
       }
       for (uint32_t k = 0; k < kend; ++k) {
         const uint32_t d = fd.dfa_first + k;
         if constexpr (kReg < 0) {
-          if (c.dds[d].kind == kDfaSearch) {  // a run of search automata, four at a time
+          if (c.dds[d].kind == kDfaSearch && k + 1 < kend && c.dds[d + 1].kind == kDfaSearch) {
+            // a run of search automata, four at a time (a single one below:
+            // walk_search, which reads an LDS-resident table from LDS)
             uint32_t m = 1;
-            while (m < 4 && k + m < fd.ndfa && c.dds[d + m].kind == kDfaSearch) ++m;
+            while (m < 4 && k + m < kend && c.dds[d + m].kind == kDfaSearch) ++m;
             uint32_t out[4];
-            walk_search4(c, d, m, src, p, len, out);
+            walk_search4<false>(c, d, m, src, p, len, out);
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
               if (j < m) codes.set(d + j, out[j]);
@@ -1379,7 +1431,7 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
         prof[q] = o2 > prof[q] ? o2 : prof[q];
       }
     if (lane == 0)
-      printf("L7M_PROF validate %llu jobsel %llu walks %llu setcode %llu tail %llu verify %llu eval %llu\n",
+      printf("L7M_PROF validate %llu jobsel %llu walks %llu setcode %llu tail %llu gram %llu eval %llu\n",
              (unsigned long long)prof[1], (unsigned long long)prof[2], (unsigned long long)prof[3],
              (unsigned long long)prof[4], (unsigned long long)prof[5], (unsigned long long)prof[6],
              (unsigned long long)prof[7]);
@@ -1404,15 +1456,28 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
 }
 
 // Second pass over the requests the first pass deferred (a slow-path rule may
-// decide them, program.h kCrSlow): one lane per queued request, records read
-// from HBM, the same walk phase, then verification with the slow-path
-// executor (regex_vm.h) on this lane's scratch.  Two tiers (regex_vm.h): tier
-// 1 runs every deferred request on a 32 KiB scratch over one wave per CU;
-// requests it could not decide (stack or step budget) are queued for tier 2,
-// kSlowLanes2 lanes with 1 MiB each.  Verdicts and counters of these requests
-// are written here only.
-constexpr uint32_t kSlowBlock = 64;     // one wave per workgroup (and per CU)
-constexpr uint32_t kSlowBlocks2 = 4;    // tier 2: 256 lanes x 1 MiB
+// decide them, program.h kCrSlow): one lane per queued request, the same walk
+// phase, then verification with the slow-path executor (regex_vm.h) on this
+// lane's scratch.  Each wave takes the next 64 queued requests from a work
+// counter and copies every record that fits kSlowRec bytes into its lane's
+// LDS slot (walk and executor then read LDS; larger records are read from
+// HBM).  Two tiers (regex_vm.h): tier 1 runs every deferred request with 16
+// KiB of executor stack, kSlowWavesPerCu waves per CU; requests it could not
+// decide (stack or step budget) are queued for tier 2, kSlowBlocks2 waves
+// with 1 MiB per lane.  Verdicts and counters of these requests are written
+// here only.
+constexpr uint32_t kSlowBlock = 64;       // one wave per workgroup
+constexpr uint32_t kSlowWavesPerCu = 4;   // tier 1
+constexpr uint32_t kSlowBlocks2 = 4;      // tier 2: 256 lanes x 1 MiB
+constexpr uint32_t kSlowRec = 256;        // LDS record slot per lane (records <= kSlowRec - 32 bytes)
+
+// LDS of one slow-pass workgroup: the table image, the end-code columns
+// (Codes<0>, first-pass stride), the record slots.
+size_t http_slow_lds_bytes(const HttpHeader& h, bool reg) {
+  return 4u * (static_cast<size_t>(h.lds_image_words) + (reg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock)) +
+         static_cast<size_t>(kSlowBlock) * kSlowRec;
+}
+
 template <int kReg, bool kLit, int kTier>
 __global__ __launch_bounds__(kSlowBlock) void http_slow_kernel(const uint32_t* __restrict__ prog,
                                                                const uint8_t* __restrict__ arena, uint64_t arena_bytes,
@@ -1421,7 +1486,8 @@ __global__ __launch_bounds__(kSlowBlock) void http_slow_kernel(const uint32_t* _
                                                                unsigned long long* __restrict__ hits,
                                                                const uint32_t* __restrict__ slowq,
                                                                uint32_t* __restrict__ slowq2,
-                                                               uint32_t* __restrict__ vmscratch) {
+                                                               uint32_t* __restrict__ vmscratch,
+                                                               uint32_t* __restrict__ work) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x;
@@ -1442,30 +1508,54 @@ __global__ __launch_bounds__(kSlowBlock) void http_slow_kernel(const uint32_t* _
   c.pool = prog + h.off_pool;
   c.cr = prog + h.off_cr;
   c.remotes = reinterpret_cast<const Span*>(prog + h.off_remotes);
+  uint32_t* slot = img + h.lds_image_words + (kReg ? 0u : h.n_dfas * kBlock) + tid * (kSlowRec / 4);
   const uint32_t gtid = blockIdx.x * kSlowBlock + tid;
   uint32_t* vm = vmscratch + static_cast<uint64_t>(gtid) * (kTier == 1 ? kVmScratchWords : kVmScratchWords2);
   const uint32_t* q_in = kTier == 1 ? slowq : slowq2;
   const uint32_t nq = q_in[0];
   uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t q = gtid; q < nq; q += gridDim.x * kSlowBlock) {
-    const uint32_t ri = q_in[1 + q];
-    if (ri >= n) continue;
-    const uint64_t o = offs[ri];
-    WalkOut<kReg> wo;
-    if constexpr (!kReg) wo.codes.p = img + h.lds_image_words + tid;
-    int32_t v = L7M_VERDICT_PARSE_ERROR;
-    const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
-    const GlbSrc src{reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0))};
-    if (inb) v = eval_walk<kReg, 0, kLit>(c, h, src, arena_bytes - o, wo, prof);
-    if (v == kNeedVerify) v = eval_verify<kReg, kTier>(c, h, wo, &src, vm);
-    if (kTier == 1 && v == kDeferred2) {  // the large-stack tier decides it
-      const uint32_t at = atomicAdd(slowq2, 1u);
-      slowq2[1 + at] = ri;
-      continue;
+  for (;;) {
+    uint32_t base = 0;
+    if (tid == 0) base = atomicAdd(work, kSlowBlock);
+    base = __shfl(base, 0);
+    if (base >= nq) break;
+    const uint32_t q = base + tid;
+    const uint32_t ri = q < nq ? q_in[1 + q] : kNone;
+    int32_t v = kDeferred;  // (inactive lanes)
+    if (ri < n) {
+      const uint64_t o = offs[ri];
+      WalkOut<kReg> wo;
+      if constexpr (!kReg) wo.codes.p = img + h.lds_image_words + tid;
+      v = L7M_VERDICT_PARSE_ERROR;
+      const bool inb = (o & 3) == 0 && o + L7M_HTTP_REC_FIXED <= arena_bytes;
+      const uint32_t* rw = reinterpret_cast<const uint32_t*>(arena + (inb ? o : 0));
+      const uint32_t rlen = inb ? ((rw[0] + 3u) & ~3u) : 0u;
+      if (inb && rlen <= kSlowRec - 32 && o + rlen <= arena_bytes) {
+        // the record into this lane's LDS slot (16-byte loads; the slack past
+        // it is zero so over-reads see no stale bytes)
+        const uint4* g = reinterpret_cast<const uint4*>(rw);
+        uint4* l = reinterpret_cast<uint4*>(slot);
+        for (uint32_t i = 0; i < (rlen + 15) / 16 + 1; ++i) l[i] = 16 * i < rlen ? g[i] : uint4{0, 0, 0, 0};
+        const LdsSrc src{slot};
+        v = eval_walk<kReg, 0, kLit>(c, h, src, rlen, wo, prof);
+        if (v == kNeedVerify) v = eval_verify<kReg, kTier>(c, h, wo, &src, vm);
+      } else if (inb) {
+        const GlbSrc src{rw};
+        v = eval_walk<kReg, 0, kLit>(c, h, src, arena_bytes - o, wo, prof);
+        if (v == kNeedVerify) v = eval_verify<kReg, kTier>(c, h, wo, &src, vm);
+      }
+      if (kTier == 1 && v == kDeferred2) {  // the large-stack tier decides it
+        const uint32_t at = atomicAdd(slowq2, 1u);
+        slowq2[1 + at] = ri;
+        v = kDeferred;
+      }
+      if (v != kDeferred) verdicts[ri] = v;
     }
-    verdicts[ri] = v;
-    if (hits && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY)
-      atomicAdd(hits + (v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u)), 1ull);
+    if (hits) {
+      const bool cnt = v != kDeferred && v < L7M_VERDICT_ALLOW_NO_PORT_POLICY;
+      const uint32_t sl = v >= 0 ? static_cast<uint32_t>(v) + 2u : (v == L7M_VERDICT_DENY ? 0u : 1u);
+      count_slot(hits, cnt ? sl : 0u, cnt);
+    }
   }
 }
 
@@ -1506,14 +1596,14 @@ template <int kReg, bool kLit, int kTier>
 static hipError_t launch_slow(const HttpHeader& h, uint32_t blocks, hipStream_t stream, const uint32_t* dprog,
                               const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs, uint64_t n,
                               int32_t* verdicts, unsigned long long* hits, const uint32_t* slowq, uint32_t* slowq2,
-                              uint32_t* vmscratch) {
-  // LDS code columns keep the first pass's stride (Codes<0>: kBlock)
-  const size_t lds = 4u * (static_cast<size_t>(h.lds_image_words) + (kReg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock));
+                              uint32_t* vmscratch, uint32_t* work) {
+  const size_t lds = http_slow_lds_bytes(h, kReg != 0);
+  if (lds > kHttpLdsBytes) return hipErrorInvalidValue;
   const hipError_t e =
       set_lds_attr_once(reinterpret_cast<const void*>(http_slow_kernel<kReg, kLit, kTier>), kHttpLdsBytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_slow_kernel<kReg, kLit, kTier>), dim3(blocks), dim3(kSlowBlock), lds, stream, dprog, arena,
-                     arena_bytes, offs, n, verdicts, hits, slowq, slowq2, vmscratch);
+                     arena_bytes, offs, n, verdicts, hits, slowq, slowq2, vmscratch, work);
   return hipGetLastError();
 }
 
@@ -1570,25 +1660,28 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   uint32_t* slowq2 = nullptr;
   uint32_t* vms = nullptr;
   uint32_t* vms2 = nullptr;
+  uint32_t* work = nullptr;  // [0] tier-1, [64] tier-2 work counters
   const size_t qbytes = (4ull * (n + 1) + 255) & ~size_t(255);
-  // tier 1: one wave per CU (fewer for small batches), tier 2: kSlowBlocks2 waves
+  // tier 1: kSlowWavesPerCu waves per CU (fewer for small batches), tier 2: kSlowBlocks2 waves
   const uint64_t waves = (n + kSlowBlock - 1) / kSlowBlock;
-  const uint64_t cus = num_cus > 0 ? static_cast<uint64_t>(num_cus) : 256u;
-  const uint32_t blocks1 = static_cast<uint32_t>(waves < cus ? waves : cus);
+  const uint64_t w1 = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * kSlowWavesPerCu;
+  const uint32_t blocks1 = static_cast<uint32_t>(waves < w1 ? waves : w1);
   const uint32_t blocks2 = static_cast<uint32_t>(waves < kSlowBlocks2 ? waves : kSlowBlocks2);
   if (h.n_slow) {
     void* buf = nullptr;
     const size_t v1 = static_cast<size_t>(blocks1) * kSlowBlock * kVmScratchWords * 4u;
     const size_t v2 = static_cast<size_t>(blocks2) * kSlowBlock * kVmScratchWords2 * 4u;
     keep_stream_pool();
-    hipError_t e = hipMallocAsync(&buf, 2 * qbytes + v1 + v2, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(buf, 0, 4, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(buf) + qbytes, 0, 4, stream);
+    hipError_t e = hipMallocAsync(&buf, 512 + 2 * qbytes + v1 + v2, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(buf, 0, 512, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(buf) + 512, 0, 4, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(buf) + 512 + qbytes, 0, 4, stream);
     if (e != hipSuccess) return e;
-    slowq = static_cast<uint32_t*>(buf);
-    slowq2 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + qbytes);
-    vms = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 2 * qbytes);
-    vms2 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 2 * qbytes + v1);
+    work = static_cast<uint32_t*>(buf);
+    slowq = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 512);
+    slowq2 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 512 + qbytes);
+    vms = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 512 + 2 * qbytes);
+    vms2 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 512 + 2 * qbytes + v1);
   }
   hipError_t e = hipSuccess;
 #define L7M_LAUNCH(M, RR)                                                                                          \
@@ -1610,9 +1703,9 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   if (h.n_slow) {
 #define L7M_SLOW(RR, T, B, V)                                                                                      \
   e = lit ? launch_slow<RR, true, T>(h, B, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq, slowq2, \
-                                     V)                                                                            \
+                                     V, work + (T - 1) * 64)                                                       \
           : launch_slow<RR, false, T>(h, B, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, slowq,      \
-                                      slowq2, V)
+                                      slowq2, V, work + (T - 1) * 64)
     for (int tier = 1; tier <= 2 && e == hipSuccess; ++tier) {
       if (tier == 1) {
         if (R == 4) L7M_SLOW(4, 1, blocks1, vms);

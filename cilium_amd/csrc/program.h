@@ -82,7 +82,9 @@ struct DfaDesc {
   uint32_t acc_cmap_off; // kDfaSearch: program word offset of the 256-byte byte -> class map
   uint32_t acc_mid_off;  // kDfaSearch: program: u32 pattern mask per mid-set id (256)
   uint32_t acc_ncls;     // kDfaSearch: byte classes (row length of the dense table)
-  uint32_t pad[4];       // 128 bytes: descriptor addresses are a shift of the DFA index
+  uint32_t lds_search;   // kDfaSearch: LDS image word offset of the dense table (small automata), or kNone
+  uint32_t lds_mid;      // kDfaSearch: LDS image word offset of its mid masks, or kNone
+  uint32_t pad[2];       // 128 bytes: descriptor addresses are a shift of the DFA index
 };
 static_assert(sizeof(DfaDesc) == 128, "dfa desc is 32 words");
 
@@ -97,6 +99,7 @@ static_assert(sizeof(DfaDesc) == 128, "dfa desc is 32 words");
 // the rules keyed on pattern p.
 constexpr uint32_t kDfaPacked = 0, kDfaSearch = 1;
 constexpr uint32_t kSearchMaxPats = 32, kSearchMaxMid = 256;
+constexpr uint32_t kLdsSearchMaxWords = 2048;  // search tables up to 8 KiB are walked from LDS
 
 // Candidate entry of one end code (16 words): the keyed rules' check records
 // (sorted by rule id) live in the check-record pool at [off, len records);
@@ -163,7 +166,7 @@ static_assert(sizeof(FieldDesc) == 32, "field desc is 8 words");
 // Every match of a pattern contains its required literal (regex_re2.cc
 // required_literals), so a value lacking all of a group's chosen 4-byte grams
 // cannot match any of the group's patterns.
-constexpr uint32_t kGramMinGroups = 3;      // fields with fewer search groups walk them all
+constexpr uint32_t kGramMinGroups = 2;      // fields with fewer search groups walk them all
 constexpr uint32_t kGramMaxGroups = 64;
 __host__ __device__ inline uint32_t gram_bucket(uint32_t gram) { return (gram * 0x9e3779b1u) >> 16; }
 

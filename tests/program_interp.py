@@ -35,7 +35,7 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search pair_pa off_slow n_slow").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab "
-              "lds_skip skip_lim kind acc_cmap_off acc_mid_off acc_ncls").split()
+              "lds_skip skip_lim kind acc_cmap_off acc_mid_off acc_ncls lds_search lds_mid").split()
 ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 DFA_WORDS = 32  # sizeof(DfaDesc) / 4
 DFA_SEARCH = 1  # program.h kDfaSearch

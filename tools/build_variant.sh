@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 NAME=$1; FLAGS=${2:-}
 B=cilium_amd/csrc/build_$NAME
 mkdir -p $B variants
-for f in regex_ecma regex_re2 regex_vm dfa_pack http_compile kafka_compile l7m_api l7m_side l7m_batch; do
+for f in regex_ecma regex_re2 regex_vm dfa_pack http_compile kafka_compile l7m_api l7m_side l7m_batch l7m_multi; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-result $FLAGS -D__HIP_PLATFORM_AMD__ \
     -I/opt/rocm/include -x c++ -c cilium_amd/csrc/$f.cc -o $B/$f.o &
 done
@@ -16,5 +16,5 @@ for f in l7m_kernels l7m_kafka; do
     -munsafe-fp-atomics -c cilium_amd/csrc/$f.hip -o $B/$f.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o variants/$NAME.so $B/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o variants/$NAME.so $B/*.o -ldl
 echo "built variants/$NAME.so"
