@@ -135,7 +135,116 @@ struct Group {
   PackedDfa pk;                // kDfaPacked groups
   bool search = false;         // kDfaSearch group (sd)
   SearchDfa sd;
+  bool alit = false;           // kDfaAlit group (no automaton: the field's alit scan)
 };
+
+// Literal-anchored RE2 patterns of one field (program.h FieldDesc::alit_*).
+struct AlitField {
+  bool on = false;
+  uint32_t first_group = 0;            // field group index of the first kDfaAlit group
+  std::vector<uint32_t> tab;           // buckets x {gram, pattern + 1, gram, pattern + 1}
+  std::vector<uint32_t> pats;          // field pattern ids in alit order (AlitPat index)
+  std::vector<std::string> lit;        // per alit pattern: L
+  std::vector<uint32_t> k;             // per alit pattern: offset of its table gram in L
+  std::vector<uint32_t> resid;         // per alit pattern: residual id, kNone = empty
+  PackedDfa resid_pk;                  // automaton of the distinct residuals
+  uint32_t n_resid = 0;
+};
+
+// Choose the alit patterns of a field: every RE2 pattern L R whose L's
+// grams fit the table (rarest gram first); the rest stay search patterns.
+void plan_alit(const std::vector<re::Ast>& asts, const std::vector<uint32_t>& sidx, AlitField* out,
+               std::vector<uint32_t>* rest) {
+  std::vector<uint32_t> cand;
+  std::vector<std::string> lits;
+  std::vector<re::Ast> res;
+  for (uint32_t p : sidx) {
+    re::Ast sa = asts[p];
+    re::simplify_search(&sa);
+    std::string L;
+    re::Ast R;
+    if (re::split_literal_prefix(sa, &L, &R)) {
+      cand.push_back(p);
+      lits.push_back(std::move(L));
+      res.push_back(std::move(R));
+    } else {
+      rest->push_back(p);
+    }
+  }
+  if (cand.size() < kAlitMinPatterns) {
+    rest->insert(rest->end(), cand.begin(), cand.end());
+    std::sort(rest->begin(), rest->end());
+    return;
+  }
+  std::map<uint32_t, uint32_t> freq;
+  for (const auto& L : lits)
+    for (size_t i = 0; i + 4 <= L.size(); ++i) {
+      uint32_t g;
+      std::memcpy(&g, L.data() + i, 4);
+      ++freq[g];
+    }
+  uint32_t buckets = 64;
+  while (buckets < cand.size()) buckets <<= 1;
+  if (16ull * buckets > kAlitMaxLdsBytes) buckets = kAlitMaxLdsBytes / 16;
+  out->tab.assign(4ull * buckets, 0u);
+  std::map<std::string, uint32_t> rid;
+  std::vector<re::Ast> rasts;
+  for (size_t c = 0; c < cand.size(); ++c) {
+    const std::string& L = lits[c];
+    int best_i = -1, best_e = -1;
+    uint32_t best_f = kNone, best_g = 0;
+    for (size_t i = 0; i + 4 <= L.size(); ++i) {
+      uint32_t g;
+      std::memcpy(&g, L.data() + i, 4);
+      const uint32_t* b = &out->tab[4ull * (gram_bucket(g) & (buckets - 1))];
+      const int e = !b[1] ? 0 : !b[3] ? 1 : -1;
+      if (e < 0) continue;
+      if (freq[g] < best_f) {
+        best_f = freq[g];
+        best_i = static_cast<int>(i);
+        best_e = e;
+        best_g = g;
+      }
+    }
+    if (best_i < 0) {  // every bucket of its grams is full: a search pattern
+      rest->push_back(cand[c]);
+      continue;
+    }
+    const uint32_t id = static_cast<uint32_t>(out->pats.size());
+    uint32_t* b = &out->tab[4ull * (gram_bucket(best_g) & (buckets - 1))];
+    b[2 * best_e] = best_g;
+    b[2 * best_e + 1] = id + 1;
+    out->pats.push_back(cand[c]);
+    out->lit.push_back(L);
+    out->k.push_back(static_cast<uint32_t>(best_i));
+    if (re::residual_is_empty(res[c])) {
+      out->resid.push_back(kNone);
+    } else {
+      auto it = rid.emplace(re::ast_key(res[c]), static_cast<uint32_t>(rasts.size()));
+      if (it.second) rasts.push_back(std::move(res[c]));
+      out->resid.push_back(it.first->second);
+    }
+  }
+  std::sort(rest->begin(), rest->end());
+  if (out->pats.size() < kAlitMinPatterns) {
+    rest->insert(rest->end(), out->pats.begin(), out->pats.end());
+    std::sort(rest->begin(), rest->end());
+    *out = AlitField();
+    return;
+  }
+  out->n_resid = static_cast<uint32_t>(rasts.size());
+  if (!rasts.empty()) {
+    std::vector<const re::Ast*> rp;
+    for (const auto& a : rasts) rp.push_back(&a);
+    if (build_field_dfa(rp, FieldDfaLimits(), &out->resid_pk) != re::Status::Ok || out->resid_pk.n_slots > 12000) {
+      rest->insert(rest->end(), out->pats.begin(), out->pats.end());  // residual automaton too large: search groups
+      std::sort(rest->begin(), rest->end());
+      *out = AlitField();
+      return;
+    }
+  }
+  out->on = true;
+}
 
 // Search groups of one field's RE2-dialect patterns: chunks of
 // kSearchMaxPats, halved while an automaton exceeds the limits.
@@ -185,6 +294,7 @@ struct GramFilter {
   bool on = false;
   uint32_t search_first = 0;  // field group index of the first search group
   uint32_t always = 0;        // groups walked for every value
+  uint32_t n_search = 0;      // search groups of the field
   std::vector<uint32_t> tab;  // buckets x {gram, mask, gram, mask}
 };
 
@@ -396,6 +506,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   // field pattern -> (group, local id)
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fp_loc(nf);
   std::vector<GramFilter> gram(nf);  // RE2 dialect: per field, which search groups a value may need
+  std::vector<AlitField> alit(nf);   // RE2 dialect: per field, the literal-anchored patterns
   for (uint32_t f = 0; f < nf; ++f) {
     if (fpats[f].empty()) continue;
     std::vector<re::Ast> asts(fpats[f].size());
@@ -464,6 +575,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
     }
     if (!sidx.empty()) {
+      // literal-anchored patterns (L R) leave the search groups: an alit scan
+      // decides them (gram probe, literal compare, shared residual automaton)
+      {
+        std::vector<uint32_t> rest;
+        plan_alit(asts, sidx, &alit[f], &rest);
+        sidx = std::move(rest);
+      }
       // patterns without a 4-byte required literal ("always" walked) are
       // grouped apart from the others, so the gram filter can skip whole groups
       std::vector<std::vector<uint32_t>> grams(fpats[f].size());
@@ -480,7 +598,10 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
         (grams[p].empty() ? s_always : s_lit).push_back(p);
       }
       const uint32_t first = static_cast<uint32_t>(groups[f].size());
-      if (sidx.size() <= kSearchMaxPats) {  // one group: walked anyway, no filter
+      gram[f].search_first = first;
+      if (sidx.empty()) {
+        // every regex of the field is literal-anchored
+      } else if (sidx.size() <= kSearchMaxPats && !alit[f].on) {  // one group: walked anyway, no filter
         int rc = build_search_groups(ptrs, sidx, &groups[f], &err);
         if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
         gram[f].search_first = first;
@@ -495,6 +616,16 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
           if (rc != L7M_OK) return fail(rc, field_names[f] + ": " + err);
         }
         build_gram_filter(groups[f], first, first_lit, grams, &gram[f]);
+      }
+      gram[f].n_search = static_cast<uint32_t>(groups[f].size()) - first;
+    }
+    if (alit[f].on) {  // kDfaAlit groups of <= kSearchMaxPats patterns, after the search groups
+      alit[f].first_group = static_cast<uint32_t>(groups[f].size());
+      for (size_t o = 0; o < alit[f].pats.size(); o += kSearchMaxPats) {
+        Group g;
+        g.alit = true;
+        g.pats.assign(alit[f].pats.begin() + o, alit[f].pats.begin() + std::min(alit[f].pats.size(), o + kSearchMaxPats));
+        groups[f].push_back(std::move(g));
       }
     }
     fp_loc[f].assign(fpats[f].size(), {0, 0});
@@ -644,6 +775,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   for (uint32_t f = 0; f < nf; ++f)
     for (auto& g : groups[f]) all.push_back({&g.pk, f, static_cast<uint32_t>(g.pats.size()), &g});
   if (has_name) all.push_back({&name_dfa, kNone, nf - 3, nullptr});
+  // the literal-anchored fields' residual automata (after the name DFA)
+  std::vector<uint32_t> resid_dfa(nf, kNone);
+  for (uint32_t f = 0; f < nf; ++f)
+    if (alit[f].on && alit[f].n_resid) {
+      resid_dfa[f] = static_cast<uint32_t>(all.size());
+      all.push_back({&alit[f].resid_pk, f, alit[f].n_resid, nullptr});
+    }
   const uint32_t ndt = static_cast<uint32_t>(all.size());
 
   std::vector<DfaDesc> dd(ndt);
@@ -670,6 +808,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     dd[k].skip_lim = 0;
     dd[k].kind = kDfaPacked;
     dd[k].lds_search = dd[k].lds_mid = kNone;
+    if (all[k].grp && all[k].grp->alit) {  // no automaton: codes from the field's alit scan
+      dd[k].kind = kDfaAlit;
+      dd[k].start_base = 0;
+      dd[k].region = 0;
+      dd[k].n_slots = 0;
+      dd[k].nstates = 0;
+    }
     if (all[k].grp && all[k].grp->search) {
       const SearchDfa& sd = all[k].grp->sd;
       dd[k].kind = kDfaSearch;
@@ -715,6 +860,11 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     fd[f].gram_mask = 0;
     fd[f].always = ~0u;
     fd[f].search_first = gram[f].search_first;
+    fd[f].n_search = gram[f].n_search;
+    fd[f].alit_tab = fd[f].alit_pats = kNone;
+    fd[f].alit_mask = 0;
+    fd[f].alit_lds = 0;
+    fd[f].resid_dfa = resid_dfa[f];
   }
   std::vector<Span> rremote(n);
   for (size_t i = 0; i < n; ++i) rremote[i] = push_list(remotes[i]);
@@ -773,6 +923,16 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       for (uint32_t f = 3; f < nf; ++f) name_off.push_back(img_take((field_names[f].size() + 3) / 4));
     }
   }
+  // RE2-dialect literal-anchored patterns: the bucket table (read once per
+  // value byte; their groups have no automaton, so it must be resident)
+  for (uint32_t f = 0; f < nf; ++f) {
+    if (!alit[f].on) continue;
+    if (img + alit[f].tab.size() > budget)
+      return fail(L7M_ETOOBIG, field_names[f] + ": the literal-anchored pattern table needs " +
+                                   std::to_string(4 * alit[f].tab.size()) + " bytes of LDS");
+    fd[f].alit_tab = img_take(alit[f].tab.size());
+    fd[f].alit_mask = static_cast<uint32_t>(alit[f].tab.size() / 4 - 1);
+  }
   // RE2-dialect gram filters (read once per value byte): right after the name table
   for (uint32_t f = 0; f < nf; ++f) {
     if (!gram[f].on || img + gram[f].tab.size() > budget) continue;
@@ -786,6 +946,22 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     if (!all[k].grp || !all[k].grp->search) continue;
     const uint64_t mw = all[k].grp->sd.midmask.size();
     if (img + ((mw + 3) & ~3ull) <= budget) dd[k].lds_mid = img_take(mw);
+  }
+  // ... the residual automata they walk (slot table + end codes, pattern masks)
+  for (uint32_t f = 0; f < nf; ++f) {
+    const uint32_t k = resid_dfa[f];
+    if (k == kNone || fd[f].alit_tab == kNone) continue;
+    const PackedDfa& d = *all[k].d;
+    const uint64_t half_latch = (d.latch.size() + 1) / 2;
+    const bool es8 = d.sets.size() < kEs8Latched && all[k].npats < kEs16Latched;
+    if (es8 && img + d.n_slots <= kLdsTableWords &&
+        img + ((d.n_slots + 3) & ~3ull) + ((half_latch + 3) & ~3ull) <= budget) {
+      dd[k].lds_table = img_take(d.n_slots);
+      dd[k].lds_es = kLdsEsInEntry;
+      dd[k].lds_latch = 2 * img_take(half_latch);
+    }
+    if (!masks[k].empty() && img + ((2 * masks[k].size() + 3) & ~size_t(3)) <= budget)
+      dd[k].lds_mask = img_take(2 * masks[k].size());
   }
   // (policy, direction, port) -> port entry table (open addressing on
   // ent_hash, program.h); in LDS when small
@@ -818,6 +994,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   for (uint32_t k = 0; k < ndt; ++k) order[k] = k;
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hotness(a) < hotness(b); });
   for (uint32_t k : order) {
+    if (dd[k].kind == kDfaAlit || dd[k].lds_table != kNone) continue;  // no automaton / placed above
     if (dd[k].kind == kDfaSearch) {  // walked from the program; the 256-byte class map in LDS when it fits
       if (img + 64 <= budget) dd[k].lds_table = img_take(64);
       // small automata (a method's, a few hosts'): the dense table and its mid
@@ -854,7 +1031,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   // more (measured on MI355X, config 2: 5.0 ms with them in HBM vs 5.5 ms).
   const uint64_t ct_budget = std::min<uint64_t>(budget, kLdsCtBudget / 4);
   for (uint32_t k : order) {
-    if (!masks[k].empty() && img + ((2 * masks[k].size() + 3) & ~size_t(3)) <= budget)
+    if (!masks[k].empty() && dd[k].lds_mask == kNone && img + ((2 * masks[k].size() + 3) & ~size_t(3)) <= budget)
       dd[k].lds_mask = img_take(2 * masks[k].size());
   }
   for (uint32_t k : order) {
@@ -862,6 +1039,25 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       dd[k].lds_ct = img_take(16 * ct[k].size());
   }
 
+  // literal-anchored patterns' descriptors and literals, last: in LDS when they fit
+  // (else program memory)
+  std::vector<std::vector<uint32_t>> alit_lit_off(nf);
+  for (uint32_t f = 0; f < nf; ++f) {
+    if (fd[f].alit_tab == kNone) continue;
+    uint64_t words = 4ull * alit[f].pats.size();
+    for (const auto& L : alit[f].lit) words += ((L.size() + 3) / 4 + 1 + 3) & ~3ull;
+    // (read once per candidate, but an L2 round trip each from the program:
+    // they may exceed the table budget by kAlitExtraLdsBytes)
+#ifdef L7M_ALIT_NO_LDS
+    continue;
+#endif
+    if (img + words > budget + kAlitExtraLdsBytes / 4 || 4 * (img + words) + codes_bytes + ctr_bytes +
+                                                                 stage_bytes > kHttpLdsBytes)
+      continue;
+    fd[f].alit_lds = 1;
+    fd[f].alit_pats = img_take(4ull * alit[f].pats.size());
+    for (const auto& L : alit[f].lit) alit_lit_off[f].push_back(img_take((L.size() + 3) / 4 + 1));
+  }
   // ---- program layout ----
   HttpHeader h;
   std::memset(&h, 0, sizeof h);
@@ -934,7 +1130,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       slow_span[i].len /= 2;  // pairs
     }
   }
-  for (uint32_t k = 0; k < ndfa; ++k) h.search |= dd[k].kind == kDfaSearch ? 1u : 0u;
+  for (uint32_t k = 0; k < ndfa; ++k) h.search |= dd[k].kind != kDfaPacked ? 1u : 0u;
   h.ent_mask = ent_slots - 1;
   h.ent_tab_off = take(2ull * ent_slots);
   h.off_pool = take(pool.size());
@@ -946,6 +1142,8 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       dd[k].latch_off = take(0);
       dd[k].acc_cmap_off = take(256 / 4);
       dd[k].acc_mid_off = take(kSearchMaxMid);
+    } else if (dd[k].kind == kDfaAlit) {
+      dd[k].table_off = dd[k].es_off = dd[k].latch_off = take(0);
     } else {
       dd[k].table_off = take(all[k].d->n_slots);
       dd[k].es_off = take(all[k].d->n_slots);
@@ -978,6 +1176,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       lw[2 * l] = take((fp.value.size() + 3) / 4);
       lw[2 * l + 1] = static_cast<uint32_t>(fp.value.size());
     }
+  }
+  // literal-anchored patterns: AlitPat[] and the literals (program memory)
+  // when the LDS image has no room for them
+  for (uint32_t f = 0; f < nf; ++f) {
+    if (fd[f].alit_tab == kNone || fd[f].alit_lds) continue;
+    fd[f].alit_pats = take(4ull * alit[f].pats.size());
+    for (const auto& L : alit[f].lit) alit_lit_off[f].push_back(take((L.size() + 3) / 4 + 1));  // + a zero word
   }
   w = (w + 63) & ~uint64_t(63);  // 256-byte aligned image
   h.lds_image_off = take(img);
@@ -1063,6 +1268,22 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   std::memcpy(I + lds_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
   for (uint32_t f = 0; f < nf; ++f)
     if (fd[f].gram_tab != kNone) std::memcpy(I + fd[f].gram_tab, gram[f].tab.data(), gram[f].tab.size() * 4ull);
+  for (uint32_t f = 0; f < nf; ++f) {
+    if (fd[f].alit_tab == kNone) continue;
+    const AlitField& A = alit[f];
+    std::memcpy(I + fd[f].alit_tab, A.tab.data(), A.tab.size() * 4ull);
+    for (size_t i = 0; i < A.pats.size(); ++i) {
+      const auto loc = fp_loc[f][A.pats[i]];  // (group, local id)
+      AlitPat ap;
+      ap.lit = alit_lit_off[f][i];
+      ap.len_k = static_cast<uint32_t>(A.lit[i].size()) | A.k[i] << 16;
+      ap.code = (dfa_first[f] + loc.first) << 8 | loc.second;
+      ap.resid = A.resid[i];
+      uint32_t* base = fd[f].alit_lds ? I : P;
+      std::memcpy(base + fd[f].alit_pats + 4 * i, &ap, sizeof ap);
+      std::memcpy(reinterpret_cast<uint8_t*>(base + alit_lit_off[f][i]), A.lit[i].data(), A.lit[i].size());
+    }
+  }
   std::memcpy(P + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));
   std::memcpy(I + lds_fields, fd.data(), fd.size() * sizeof(FieldDesc));
   if (lds_name_tab != kNone) {

@@ -135,6 +135,11 @@ Req http_req_cfg2(const std::vector<HttpRuleT>& rules, uint64_t seed, uint64_t i
   if (t.host) q.authority = "svc" + std::to_string(ri % 50) + ".ns.local";
   else q.authority = r.p(0.5) ? "svc" + std::to_string(r.u(100)) + ".ns.local" : "example.com";
   fillers(r, q);
+  // config 2's mean record is ~150 B; the fillers above give
+  // ~128 B, so most requests also carry the accept-encoding header a browser
+  // or client library sends (no rule references it)
+  static const char* enc[] = {"gzip", "gzip, deflate", "gzip, deflate, br", "br", "identity", "deflate, gzip"};
+  if (r.p(0.72)) q.hdrs.push_back({"accept-encoding", enc[r.u(6)]});
   if (t.hdr == 1) q.hdrs.push_back({"x-tenant", "t" + std::to_string(ri % 17)});
   if (t.hdr == 2) q.hdrs.push_back({"x-debug", "1"});
   if (r.p(0.5)) {  // one-byte mutation of a matched field

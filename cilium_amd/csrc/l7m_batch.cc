@@ -156,6 +156,7 @@ struct l7m_batcher {
   std::vector<Batch*> pool, all;
   std::atomic<bool> stop{false};
   std::atomic<uint32_t> callers{0};
+  std::atomic<uint32_t> in_closed{0};  // callers waiting on a batch that is already being evaluated
   std::atomic<uint32_t> idle{0};  // flushers asleep
   std::mutex idle_mu;
   std::condition_variable idle_cv;
@@ -405,7 +406,12 @@ struct l7m_batcher {
         continue;
       }
       const int64_t first = b->first_ns.load();  // 0 until the first caller has stamped it
-      if (!eager && !stop.load() && cnt0 < max_batch && !b->want_close.load() &&
+      // Deadline mode flushes at max_batch, a full arena, max_delay_us after the
+      // first request -- or as soon as every caller inside l7m_batcher_eval that
+      // is not already waiting on an evaluated batch is in this one: nobody is
+      // left to join it, so waiting out the deadline would only add latency.
+      const int64_t free_callers = static_cast<int64_t>(callers.load()) - in_closed.load();
+      if (!eager && !stop.load() && cnt0 < max_batch && !b->want_close.load() && static_cast<int64_t>(cnt0) < free_callers &&
           (first == 0 || now_ns() - first < static_cast<int64_t>(max_delay_us) * 1000)) {
         cpu_relax();
         continue;
@@ -424,6 +430,7 @@ struct l7m_batcher {
         }
         s = b->resv.fetch_or(kClosed);
         cur.store(nb, std::memory_order_release);
+        in_closed.fetch_add(count_of(s));
       }
       const uint32_t cnt = count_of(s);
       const uint64_t bytes = bytes_of(s);
@@ -568,6 +575,7 @@ struct l7m_batcher {
     }
     const int rc = b->rc;
     if (rc == L7M_OK) *verdict = b->verd[idx];
+    in_closed.fetch_sub(1);
     wake_ns.fetch_add(static_cast<uint64_t>(now_ns() - b->done_ns));
     if (b->readers.fetch_sub(1) == 1) recycle(b);  // the last reader recycles the batch
     callers.fetch_sub(1);

@@ -462,6 +462,23 @@ struct Codes<-1> {
     }
     valid |= d < 64 ? 1ull << d : 0ull;
   }
+  // code |= bits (kDfaAlit groups collect their matched patterns one by one)
+  __device__ __forceinline__ void orbits(uint32_t d, uint32_t bits) {
+    bool f = false;
+#pragma unroll
+    for (uint32_t i = 0; i < kSearchRegCodes; ++i) {
+      f |= rd[i] == d;
+      rv[i] |= rd[i] == d ? bits : 0u;
+    }
+    if (f) return;
+    if ((masked && !((valid >> d) & 1ull)) || nr < kSearchRegCodes) {
+      set(d, bits | get(d));
+      return;
+    }
+    const uint32_t v = __hip_atomic_load(p + d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + d * stride, v | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    valid |= d < 64 ? 1ull << d : 0ull;
+  }
   __device__ __forceinline__ uint32_t get(uint32_t d) const {
     if (masked && !((valid >> d) & 1ull)) return 0u;
     uint32_t r = 0;
@@ -528,15 +545,16 @@ __device__ __forceinline__ uint32_t walk_search(const Ctx& c, const DfaDesc& dd,
 // RE2 dialect walks ~32 automata per path).
 // kL: every chain's table is in LDS (lds_search); else all are read from the
 // program (LDS-resident tables have their program copy too).
+constexpr uint32_t kSearchChains = 3;  // search automata walked at once per lane
 template <bool kL, class Src>
 __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t m, const Src& src, uint32_t pos,
-                                             uint32_t len, uint32_t (&out)[4]) {
-  const uint32_t* T[4];
-  const uint8_t* cm[4];
-  const uint32_t* mid[4];
-  uint32_t ncls[4], st[4], acc[4], cml[4], lt[4], lm[4];
+                                             uint32_t len, uint32_t (&out)[kSearchChains]) {
+  const uint32_t* T[kSearchChains];
+  const uint8_t* cm[kSearchChains];
+  const uint32_t* mid[kSearchChains];
+  uint32_t ncls[kSearchChains], st[kSearchChains], acc[kSearchChains], cml[kSearchChains], lt[kSearchChains], lm[kSearchChains];
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
+  for (uint32_t j = 0; j < kSearchChains; ++j) {
     const DfaDesc& dd = c.dds[d0 + (j < m ? j : 0u)];
     T[j] = c.prog + dd.table_off;
     cm[j] = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
@@ -551,7 +569,7 @@ __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t
   for (uint32_t k = 0; k < len; ++k) {
     const uint32_t b = src.byte(pos + k);
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
+    for (uint32_t j = 0; j < kSearchChains; ++j) {
       if (j < m) {
         const uint32_t ci = st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b);
         const uint32_t e = kL ? lld(c.img + lt[j] + ci) : gld(T[j] + ci);
@@ -561,21 +579,21 @@ __device__ __forceinline__ void walk_search4(const Ctx& c, uint32_t d0, uint32_t
     }
   }
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j)
+  for (uint32_t j = 0; j < kSearchChains; ++j)
     out[j] = j < m ? acc[j] | gld(c.prog + c.dds[d0 + j].es_off + st[j]) : 0u;
 }
 
 // The same with a per-lane DFA per chain (the gram filter's selection):
 // chain j walks DFA d[j] when j < m (m per lane).
 template <bool kL, class Src>
-__device__ __forceinline__ void walk_search4v(const Ctx& c, const uint32_t (&d)[4], uint32_t m, const Src& src,
-                                              uint32_t pos, uint32_t len, uint32_t (&out)[4]) {
-  const uint32_t* T[4];
-  const uint8_t* cm[4];
-  const uint32_t* mid[4];
-  uint32_t ncls[4], st[4], acc[4], cml[4], lt[4], lm[4];
+__device__ __forceinline__ void walk_search4v(const Ctx& c, const uint32_t (&d)[kSearchChains], uint32_t m, const Src& src,
+                                              uint32_t pos, uint32_t len, uint32_t (&out)[kSearchChains]) {
+  const uint32_t* T[kSearchChains];
+  const uint8_t* cm[kSearchChains];
+  const uint32_t* mid[kSearchChains];
+  uint32_t ncls[kSearchChains], st[kSearchChains], acc[kSearchChains], cml[kSearchChains], lt[kSearchChains], lm[kSearchChains];
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
+  for (uint32_t j = 0; j < kSearchChains; ++j) {
     const DfaDesc& dd = c.dds[d[j < m ? j : 0u]];
     T[j] = c.prog + dd.table_off;
     cm[j] = reinterpret_cast<const uint8_t*>(c.prog + dd.acc_cmap_off);
@@ -590,7 +608,7 @@ __device__ __forceinline__ void walk_search4v(const Ctx& c, const uint32_t (&d)[
   for (uint32_t k = 0; k < len; ++k) {
     const uint32_t b = src.byte(pos + k);
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
+    for (uint32_t j = 0; j < kSearchChains; ++j) {
       if (j < m) {
         const uint32_t ci = st[j] * ncls[j] + cmap_byte(cml[j], cm[j], b);
         const uint32_t e = kL ? lld(c.img + lt[j] + ci) : gld(T[j] + ci);
@@ -600,7 +618,7 @@ __device__ __forceinline__ void walk_search4v(const Ctx& c, const uint32_t (&d)[
     }
   }
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) out[j] = j < m ? acc[j] | gld(c.prog + c.dds[d[j]].es_off + st[j]) : 0u;
+  for (uint32_t j = 0; j < kSearchChains; ++j) out[j] = j < m ? acc[j] | gld(c.prog + c.dds[d[j]].es_off + st[j]) : 0u;
 }
 
 // RE2-dialect gram filter (program.h FieldDesc::gram_tab): bit j % 32 of the
@@ -631,6 +649,113 @@ __device__ __forceinline__ uint32_t gram_select(const Ctx& c, const FieldDesc& f
     for (uint32_t q = pos; q < end; ++q) probe(src.word_u(q), true);
   }
   return m;
+}
+
+template <bool kLit, bool kSearch, class Src>
+__device__ __forceinline__ uint32_t walk_dfa(const Ctx& c, uint32_t d, const Src& src, uint32_t pos, uint32_t len);
+template <bool kSearch>
+__device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code, uint32_t p);
+
+// Literal-anchored RE2 patterns of a field (program.h FieldDesc::alit_*):
+// every value position q whose 4-byte gram hits an entry of the LDS bucket
+// table names a pattern L R whose table gram sits at offset k of L; L is
+// compared at q - k (program memory, word-wise) and the residual automaton
+// is walked from the end of L; a match sets the pattern's bit in its kDfaAlit
+// group's code.  Positions are probed from aligned words (one LDS read per
+// four positions plus the bucket reads, all independent); only the lanes
+// with a hit run the compare and the residual walk.
+template <int kReg, class Src>
+__device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, const Src& src, uint32_t pos,
+                                          uint32_t len, Codes<kReg>& codes) {
+  if (len < 4) return;
+  const u32x4* tab = reinterpret_cast<const u32x4*>(c.img + fd.alit_tab);
+  const uint32_t am = fd.alit_mask, end = pos + len - 3;  // grams start in [pos, end)
+  auto candidate = [&](uint32_t pid, uint32_t q) {
+#ifdef L7M_DIAG_ALIT_NOCAND
+    codes.orbits(fd.dfa_first + fd.ndfa - 1, pid & 1u);
+    return;
+#endif
+    // descriptors and literals in LDS or the program (generic pointer: one
+    // flat read either way)
+    const uint32_t* base = fd.alit_lds ? c.img : c.prog;
+    const u32x4 ap = *reinterpret_cast<const u32x4*>(base + fd.alit_pats + 4u * pid);
+    const uint32_t ln = ap.y & 0xffffu, k = ap.y >> 16;
+    if (q < pos + k) return;
+    const uint32_t s = q - k;  // candidate start (record byte offset)
+    if (s + ln > pos + len) return;
+    const uint32_t* L = base + ap.x;
+    bool eq = true;
+    for (uint32_t i = 0; eq && i < ln; i += 4) {
+      const uint32_t lw = L[i >> 2];
+      const uint32_t sw = src.word_u(s + i);
+      const uint32_t rem = ln - i;
+      const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
+      eq = ((lw ^ sw) & m) == 0;
+    }
+    if (!eq) return;
+    if (ap.w != kNone) {
+      const uint32_t rc = walk_dfa<false, false>(c, fd.resid_dfa, src, s + ln, pos + len - (s + ln));
+      if (!code_has<false>(c, fd.resid_dfa, rc, ap.w)) return;
+    }
+    codes.orbits(ap.z >> 8, 1u << (ap.z & 31u));
+    // the pattern's candidate entry is read by verification: start its L2
+    // round trip now (as the packed walks' touch does)
+    const DfaDesc& gd = c.dds[ap.z >> 8];
+    if (gd.lds_ct == kNone) {
+      uint32_t t = gld(c.prog + gd.ct_off + 16u * (ap.z & 31u));
+      asm volatile("" ::"v"(t));
+    }
+  };
+  // The probe loop only collects hits -- (pattern, position) packed in one
+  // word -- into kAlitSlots registers; the candidates are processed after it,
+  // all lanes on their j-th candidate together, from ONE call site.
+  // (Processing each hit inside the loop ran the compare + residual walk once
+  // per word for the whole wave whenever any lane had a hit there.)  A lane
+  // whose slots fill up stops probing there; after its candidates are done it
+  // resumes at that position (outer loop).
+  constexpr uint32_t kAlitSlots = 4;
+  uint32_t from = pos;  // next position to probe
+  while (__any(from < end)) {
+    uint32_t cs[kAlitSlots], nc = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kAlitSlots; ++i) cs[i] = 0;
+    auto push = [&](bool hit, uint32_t pid, uint32_t q) {
+#pragma unroll
+      for (uint32_t i = 0; i < kAlitSlots; ++i) cs[i] = hit && nc == i ? (pid << 16 | (q - pos)) : cs[i];
+      nc += hit ? 1u : 0u;
+    };
+    uint32_t stop = end;  // first position not probed in this round
+    auto probe = [&](uint32_t g, uint32_t q) {
+      const bool on = q >= from && q < stop;
+      const u32x4 e = tab[on ? gram_bucket(g) & am : 0u];
+      const bool h0 = on && e.y && e.x == g, h1 = on && e.w && e.z == g;
+      if (nc + (h0 ? 1u : 0u) + (h1 ? 1u : 0u) > kAlitSlots) {  // no room: resume here next round
+        stop = q;
+        return;
+      }
+      push(h0, e.y - 1, q);
+      push(h1, e.w - 1, q);
+    };
+    if constexpr (Src::kLds) {
+      uint32_t q = from & ~3u;
+      uint32_t w0 = src.word(q >> 2);
+      for (; q < stop; q += 4) {
+        const uint32_t w1 = src.word((q >> 2) + 1);
+#pragma unroll
+        for (uint32_t sft = 0; sft < 4; ++sft) probe(__builtin_amdgcn_alignbyte(w1, w0, sft), q + sft);
+        w0 = w1;
+      }
+    } else {
+      for (uint32_t q = from; q < stop; ++q) probe(src.word_u(q), q);
+    }
+    for (uint32_t j = 0; j < nc; ++j) {
+      uint32_t cw = cs[0];
+#pragma unroll
+      for (uint32_t i = 1; i < kAlitSlots; ++i) cw = j == i ? cs[i] : cw;
+      candidate(cw >> 16, pos + (cw & 0xffffu));
+    }
+    from = stop;
+  }
 }
 
 template <bool kLit, bool kSearch, class Src>
@@ -691,7 +816,7 @@ template <bool kSearch>
 __device__ __forceinline__ bool code_has(const Ctx& c, uint32_t d, uint32_t code, uint32_t p) {
   if (code == 0) return false;
   const DfaDesc& dd = c.dds[d];
-  if (kSearch && dd.kind == kDfaSearch) return ((code >> p) & 1u) != 0;  // code = matched-pattern mask
+  if (kSearch && dd.kind != kDfaPacked) return ((code >> p) & 1u) != 0;  // code = matched-pattern mask
   if (code & kLatchedBit) return (code & ~kLatchedBit) == p;
   if (dd.lds_mask != kNone) {
     const uint32_t* m = c.img + dd.lds_mask + 2u * code;
@@ -853,7 +978,7 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
   auto touch = [&](uint32_t d, uint32_t code) {
     if (!touched && code && ((cand_all >> d) & 1ull)) {
       const DfaDesc& dd = c.dds[d];
-      if (dd.lds_ct == kNone && !(kReg < 0 && dd.kind == kDfaSearch)) {
+      if (dd.lds_ct == kNone && !(kReg < 0 && dd.kind != kDfaPacked)) {
         const uint32_t idx = (code & kLatchedBit) ? dd.nsets + (code & ~kLatchedBit) : code;
         pf_t = c.prog[dd.ct_off + 16u * idx];
         touched = true;
@@ -902,37 +1027,39 @@ __device__ __forceinline__ int32_t eval_walk(const Ctx& c, const HttpHeader& h, 
         if (fd.gram_tab != kNone) {
           // the search groups the value's grams select, up to four chains at a
           // time (per lane: its own groups); the packed groups before them below
-          const uint32_t sel = gram_select(c, fd, src, p, len), ns = fd.ndfa - fd.search_first;
+          const uint32_t sel = gram_select(c, fd, src, p, len), ns = fd.n_search;
           HPROF(6);  // (diagnostic build) the gram filter
           uint64_t selm = ns > 32 ? (static_cast<uint64_t>(sel) << 32 | sel) : sel;
           if (ns < 64) selm &= (1ull << ns) - 1;
           while (__any(selm != 0)) {
-            uint32_t dl[4], m = 0;
+            uint32_t dl[kSearchChains], m = 0;
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
+            for (uint32_t j = 0; j < kSearchChains; ++j) {
               dl[j] = fd.dfa_first + fd.search_first + (selm ? static_cast<uint32_t>(__builtin_ctzll(selm)) : 0u);
               m = selm ? j + 1 : m;
               selm &= selm - 1;
             }
-            uint32_t out[4];
+            uint32_t out[kSearchChains];
             walk_search4v<false>(c, dl, m, src, p, len, out);  // (LDS-resident tables keep a program copy)
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j)
+            for (uint32_t j = 0; j < kSearchChains; ++j)
               if (j < m) codes.set(dl[j], out[j]);
           }
           HPROF(3);  // gram filter + the selected groups' walks
           kend = fd.search_first;
         }
+        if (fd.alit_tab != kNone) alit_scan(c, fd, src, p, len, codes);
       }
       for (uint32_t k = 0; k < kend; ++k) {
         const uint32_t d = fd.dfa_first + k;
         if constexpr (kReg < 0) {
+          if (c.dds[d].kind == kDfaAlit) continue;  // (alit_scan)
           if (c.dds[d].kind == kDfaSearch && k + 1 < kend && c.dds[d + 1].kind == kDfaSearch) {
             // a run of search automata, four at a time (a single one below:
             // walk_search, which reads an LDS-resident table from LDS)
             uint32_t m = 1;
-            while (m < 4 && k + m < kend && c.dds[d + m].kind == kDfaSearch) ++m;
-            uint32_t out[4];
+            while (m < kSearchChains && k + m < kend && c.dds[d + m].kind == kDfaSearch) ++m;
+            uint32_t out[kSearchChains];
             walk_search4<false>(c, d, m, src, p, len, out);
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j)
@@ -1131,7 +1258,11 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
     const uint32_t code = codes.get(d);
     if (!code) continue;
     const DfaDesc& dd = c.dds[d];
-    if (kReg < 0 && dd.kind == kDfaSearch) {  // candidates of every matched pattern (entry p)
+    if (kReg < 0 && dd.kind != kDfaPacked) {  // search / alit: candidates of every matched pattern (entry p)
+#ifdef L7M_DIAG_VERIFY_SKIP
+      best = code;
+      continue;
+#endif
       for (uint32_t m = code; m; m &= m - 1) {
         const uint32_t idx = static_cast<uint32_t>(__builtin_ctz(m));
         const uint32_t mw = dd.lds_ctmask != kNone ? lld(c.img + dd.lds_ctmask + (idx >> 5))

@@ -98,6 +98,10 @@ static_assert(sizeof(DfaDesc) == 128, "dfa desc is 32 words");
 // start state, start_es8 its mid mask; nsets is 0, so candidate entry p is
 // the rules keyed on pattern p.
 constexpr uint32_t kDfaPacked = 0, kDfaSearch = 1;
+// kDfaAlit: a group of <= 32 literal-anchored RE2 patterns (FieldDesc::alit_*):
+// no table of its own, its code (the matched-pattern mask, as for kDfaSearch)
+// comes from the alit scan.
+constexpr uint32_t kDfaAlit = 2;
 constexpr uint32_t kSearchMaxPats = 32, kSearchMaxMid = 256;
 constexpr uint32_t kLdsSearchMaxWords = 2048;  // search tables up to 8 KiB are walked from LDS
 
@@ -161,12 +165,35 @@ struct FieldDesc {
   // buckets of {gram, mask, gram, mask} (mask 0 = empty entry), bucket =
   // gram_bucket(gram) & gram_mask; kNone = no filter (walk every group).
   uint32_t gram_tab, gram_mask, always, search_first;
+  uint32_t n_search;   // the gram filter's groups: [search_first, search_first + n_search)
+  // RE2-dialect literal-anchored patterns (kDfaAlit groups, after the search
+  // groups): a pattern L R (regex_ecma.h split_literal_prefix) is entered in
+  // the alit table under one 4-byte gram of L at offset k; at every value
+  // position q whose gram hits, L is compared at q - k and the residual
+  // automaton resid_dfa (one packed DFA of the field's distinct R [\x00-\xff]*)
+  // is walked from the end of L.  alit_tab: LDS image word offset of
+  // alit_mask + 1 buckets {gram, pattern + 1, gram, pattern + 1} (0 = empty),
+  // kNone = none; alit_pats: word offset of AlitPat[] -- in the LDS image
+  // when alit_lds (the literals too), else in the program (read once per
+  // candidate).
+  uint32_t alit_tab, alit_mask, alit_pats, resid_dfa;
+  uint32_t alit_lds;
+  uint32_t pad[2];
 };
-static_assert(sizeof(FieldDesc) == 32, "field desc is 8 words");
+static_assert(sizeof(FieldDesc) == 64, "field desc is 16 words");
+struct AlitPat {
+  uint32_t lit;    // word offset of L, LDS image or program as the AlitPat (zero padded + one zero word)
+  uint32_t len_k;  // |L| | k << 16 (offset of the table gram in L)
+  uint32_t code;   // kDfaAlit group DFA index << 8 | pattern bit (local id)
+  uint32_t resid;  // pattern id of R in resid_dfa, or kNone: R is empty (L decides)
+};
+constexpr uint32_t kAlitMinPatterns = 8;          // fewer: plain search groups
+constexpr uint32_t kAlitMaxLdsBytes = 32u << 10;   // the bucket table
+constexpr uint32_t kAlitExtraLdsBytes = 32u << 10; // descriptors + literals beyond the table budget
 // Every match of a pattern contains its required literal (regex_re2.cc
 // required_literals), so a value lacking all of a group's chosen 4-byte grams
 // cannot match any of the group's patterns.
-constexpr uint32_t kGramMinGroups = 2;      // fields with fewer search groups walk them all
+constexpr uint32_t kGramMinGroups = 1;      // fields with fewer search groups walk them all
 constexpr uint32_t kGramMaxGroups = 64;
 __host__ __device__ inline uint32_t gram_bucket(uint32_t gram) { return (gram * 0x9e3779b1u) >> 16; }
 

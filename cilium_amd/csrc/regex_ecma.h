@@ -112,6 +112,15 @@ void simplify_search(Ast* a);
 // literal runs of its top-level structure.  Empty when nothing is required.
 std::vector<std::string> required_literals(const Ast& a);
 
+// RE2 search patterns of the form L R (regex_re2.cc): L the literal prefix
+// (>= 4 bytes) of the top-level concatenation, R the rest, with no ^, \b or
+// look-around in R.  Under MatchString such a pattern matches iff some
+// occurrence of L in the value is followed by bytes that start with a match
+// of R; *resid = R [\x00-\xff]* (its full-match automaton answers that).
+bool split_literal_prefix(const Ast& a, std::string* lit, Ast* resid);
+bool residual_is_empty(const Ast& resid);  // R was empty: L alone decides
+std::string ast_key(const Ast& a);          // structural key (dedupes residuals)
+
 }  // namespace re
 
 // The slow path's program for a full AST (regex_vm.cc, executed by

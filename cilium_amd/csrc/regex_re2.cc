@@ -582,6 +582,95 @@ std::vector<std::string> required_literals(const Ast& a) {
   return out;
 }
 
+namespace {
+bool has_context_node(const Ast& a, int id, int depth) {
+  const Node& n = a.nodes[id];
+  if (depth > 400) return true;
+  if (n.kind == Node::Bol || n.kind == Node::WordB || n.kind == Node::Look || n.kind == Node::Backref) return true;
+  for (int k : n.kids)
+    if (has_context_node(a, k, depth + 1)) return true;
+  return false;
+}
+int copy_node(const Ast& a, int id, Ast* out) {
+  Node m = a.nodes[id];
+  for (int& k : m.kids) k = copy_node(a, k, out);
+  out->nodes.push_back(std::move(m));
+  return static_cast<int>(out->nodes.size()) - 1;
+}
+void key_of(const Ast& a, int id, std::string* k, int depth) {
+  const Node& n = a.nodes[id];
+  if (depth > 400) {
+    k->append("?");
+    return;
+  }
+  k->push_back(static_cast<char>('A' + n.kind));
+  if (n.kind == Node::Set)
+    for (int w = 0; w < 4; ++w) {
+      uint64_t v = 0;
+      for (int b = 0; b < 64; ++b)
+        if (n.set.test(64 * w + b)) v |= 1ull << b;
+      k->append(reinterpret_cast<const char*>(&v), 8);
+    }
+  if (n.kind == Node::Rep) k->append(std::to_string(n.min) + "," + std::to_string(n.max) + (n.lazy ? "l" : ""));
+  k->push_back('(');
+  for (int c : n.kids) key_of(a, c, k, depth + 1);
+  k->push_back(')');
+}
+}  // namespace
+
+bool split_literal_prefix(const Ast& a, std::string* lit, Ast* resid) {
+  const Node& r = a.nodes[a.root];
+  std::vector<int> kids;
+  if (r.kind == Node::Cat) kids = r.kids;
+  else kids.push_back(a.root);
+  lit->clear();
+  size_t i = 0;
+  for (; i < kids.size(); ++i) {
+    const Node& n = a.nodes[kids[i]];
+    if (n.kind == Node::Empty) continue;
+    if (n.kind != Node::Set || n.set.count() != 1) break;
+    for (int b = 0; b < 256; ++b)
+      if (n.set.test(b)) lit->push_back(static_cast<char>(b));
+  }
+  if (lit->size() < 4 || lit->size() > 255) return false;
+  for (size_t j = i; j < kids.size(); ++j)
+    if (has_context_node(a, kids[j], 0)) return false;
+  // the residual R, followed by anything: the pattern matches at an
+  // occurrence of L iff the bytes after it start with a match of R
+  Ast out;
+  Node cat;
+  cat.kind = Node::Cat;
+  for (size_t j = i; j < kids.size(); ++j) cat.kids.push_back(copy_node(a, kids[j], &out));
+  Node any;
+  any.kind = Node::Set;
+  any.set.set();
+  out.nodes.push_back(any);
+  Node star;
+  star.kind = Node::Rep;
+  star.kids = {static_cast<int>(out.nodes.size()) - 1};
+  star.min = 0;
+  star.max = -1;
+  out.nodes.push_back(star);
+  cat.kids.push_back(static_cast<int>(out.nodes.size()) - 1);
+  out.nodes.push_back(cat);
+  out.root = static_cast<int>(out.nodes.size()) - 1;
+  *resid = std::move(out);
+  return true;
+}
+
+bool residual_is_empty(const Ast& resid) {
+  const Node& r = resid.nodes[resid.root];
+  for (size_t j = 0; j + 1 < r.kids.size(); ++j)
+    if (resid.nodes[r.kids[j]].kind != Node::Empty) return false;
+  return true;
+}
+
+std::string ast_key(const Ast& a) {
+  std::string k;
+  key_of(a, a.root, &k, 0);
+  return k;
+}
+
 void make_search(Ast* a) {
   Node any;
   any.kind = Node::Set;

@@ -39,6 +39,7 @@ DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_
 ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 DFA_WORDS = 32  # sizeof(DfaDesc) / 4
 DFA_SEARCH = 1  # program.h kDfaSearch
+DFA_ALIT = 2    # program.h kDfaAlit
 
 
 def name_hash(data: bytes) -> int:
@@ -68,6 +69,11 @@ class HttpProgram:
         self.img = self.w[io:io + h["lds_image_words"]]
         self.img16 = prog[io:io + h["lds_image_words"]].view(np.uint16).tolist()
         ndt = h["n_dfas"] + h["has_name_dfa"]
+        # literal-anchored fields' residual automata follow the name DFA
+        for f in range(h["n_fields"]):
+            r = self.w[h["off_fields"] + 16 * f + 12]
+            if r != KNONE:
+                ndt = max(ndt, r + 1)
         self.dfas = []
         for k in range(ndt):
             o = h["lds_dfas"] + DFA_WORDS * k  # the kernel reads the LDS copy
@@ -75,10 +81,40 @@ class HttpProgram:
             g = h["off_dfas"] + DFA_WORDS * k
             assert self.w[g:g + DFA_WORDS] == self.img[o:o + DFA_WORDS]
             self.dfas.append(d)
-        # program.h FieldDesc (8 words): dfa_first, ndfa, presence off/len,
-        # gram_tab, gram_mask, always, search_first
-        self.fields = [tuple(self.img[h["lds_fields"] + 8 * f: h["lds_fields"] + 8 * f + 8])
+        # program.h FieldDesc (16 words): dfa_first, ndfa, presence off/len,
+        # gram_tab, gram_mask, always, search_first, n_search, alit_tab,
+        # alit_mask, alit_pats, resid_dfa, pad
+        self.fields = [tuple(self.img[h["lds_fields"] + 16 * f: h["lds_fields"] + 16 * f + 16])
                        for f in range(h["n_fields"])]
+        self.prog_bytes = self.prog.tobytes()
+        self.img_bytes = prog[io:io + h["lds_image_words"]].tobytes()
+
+    def alit_scan(self, f, data: bytes, codes):
+        """Literal-anchored RE2 patterns (program.h FieldDesc::alit_*): at
+        every position whose 4-byte gram hits the table, compare the
+        pattern's literal L at position - k and walk the residual automaton
+        from the end of L; matched patterns set their bit in their kDfaAlit
+        group's code."""
+        fd = self.fields[f]
+        tab, amask, pats, rdfa = fd[9], fd[10], fd[11], fd[12]
+        for q in range(len(data) - 3):
+            g = int.from_bytes(data[q:q + 4], "little")
+            b = tab + 4 * ((((g * 0x9E3779B1) & 0xFFFFFFFF) >> 16) & amask)
+            e = self.img[b:b + 4]
+            for eg, ep in ((e[0], e[1]), (e[2], e[3])):
+                if not ep or eg != g:
+                    continue
+                words, byts = (self.img, self.img_bytes) if fd[13] else (self.w, self.prog_bytes)  # alit_lds
+                lit, len_k, code, resid = words[pats + 4 * (ep - 1): pats + 4 * ep]
+                ln, k = len_k & 0xFFFF, len_k >> 16
+                s = q - k
+                if s < 0 or s + ln > len(data) or data[s:s + ln] != byts[4 * lit:4 * lit + ln]:
+                    continue
+                if resid != KNONE:
+                    rc = self.walk(rdfa, data[s + ln:])
+                    if not self.code_has(rdfa, rc, resid):
+                        continue
+                codes[code >> 8] |= 1 << (code & 31)
 
     def gram_select(self, f, data: bytes):
         """RE2-dialect gram filter (program.h FieldDesc::gram_tab): the mask
@@ -183,7 +219,7 @@ class HttpProgram:
     def code_has(self, k, code, p):
         if code == 0:
             return False
-        if self.dfas[k]["kind"] == DFA_SEARCH:
+        if self.dfas[k]["kind"] in (DFA_SEARCH, DFA_ALIT):
             return bool((code >> p) & 1)
         if code & LATCHED:
             return (code & ~LATCHED) == p
@@ -298,13 +334,18 @@ class HttpProgram:
         def eval_field(f, data):
             fvals[f] = data
             first, nd = self.fields[f][0], self.fields[f][1]
-            sf = self.fields[f][7]
+            sf, ns = self.fields[f][7], self.fields[f][8]
             sel = self.gram_select(f, data)
             for k in range(first, first + nd):
-                if sel is not None and k - first >= sf and not (sel >> ((k - first - sf) & 31)) & 1:
+                if self.dfas[k]["kind"] == DFA_ALIT:
+                    codes[k] = 0  # set by the alit scan below
+                    continue
+                if sel is not None and sf <= k - first < sf + ns and not (sel >> ((k - first - sf) & 31)) & 1:
                     codes[k] = 0  # no chosen gram of the group's patterns: not walked
                     continue
                 codes[k] = self.walk(k, data)
+            if self.fields[f][9] != KNONE:
+                self.alit_scan(f, data, codes)
 
         for f, flag, ln in ((0, L.F_METHOD, mlen), (1, L.F_PATH, plen), (2, L.F_AUTHORITY, alen)):
             if flags & flag:
@@ -372,7 +413,7 @@ class HttpProgram:
             code = codes[k]
             if not code:
                 continue
-            if self.dfas[k]["kind"] == DFA_SEARCH:  # candidates of every matched pattern
+            if self.dfas[k]["kind"] in (DFA_SEARCH, DFA_ALIT):  # candidates of every matched pattern
                 for p in range(32):
                     if (code >> p) & 1:
                         best = scan(self.ct(k, p), best)

@@ -99,7 +99,11 @@ def test_config2_1k_rules_compile_as_search_automata():
     prog = HttpProgram(rs.program())
     assert prog.h["search"] == 1
     kinds = [d["kind"] for d in prog.dfas[:prog.h["n_dfas"]]]
-    assert kinds.count(1) >= 1000 // 32
+    # search automata (kind 1) and literal-anchored groups (kind 2: every
+    # config-2 path pattern is /svc{i}/v... or /api/{w}/...: literal prefix L,
+    # residual R shared by the group)
+    assert kinds.count(1) + kinds.count(2) >= 1000 // 32
+    assert kinds.count(2) >= 1000 // 32 and prog.fields[1][9] != 0xFFFFFFFF
     arena, offs = W.requests(2, 0, 1500)
     got = prog.eval(arena, offs)
     exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
@@ -159,6 +163,7 @@ def test_gram_filter_is_exact_on_random_literal_patterns():
         prog = HttpProgram(L.RuleSet.compile_http(rules, dialect=RE2).program())
         fd = prog.fields[1]
         assert fd[4] != 0xFFFFFFFF, "path field without a gram filter"
+        assert fd[9] != 0xFFFFFFFF, "path field without literal-anchored patterns"
         reqs = [L.HTTPRequest(str(rng.choice(["GET", "PUT", "POST"])), s) for s in _gram_subjects(rng, rules, 1500)]
         arena, offs = L.pack_http(reqs)
         got = prog.eval(arena, offs)
@@ -167,4 +172,48 @@ def test_gram_filter_is_exact_on_random_literal_patterns():
         assert len(bad) == 0, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]]
         assert (exp >= 0).sum() > 100
         walked = [bin(prog.gram_select(1, r.path.encode())).count("1") for r in reqs[:300]]
-        assert np.mean(walked) < 0.5 * (fd[1] - fd[7])
+        assert np.mean(walked) < 0.5 * fd[8]
+
+
+def test_literal_anchored_patterns_exact():
+    """program.h FieldDesc::alit_*: patterns L R (literal prefix L >= 4 bytes,
+    residual R) are decided by gram probe + literal compare + the shared
+    residual automaton.  Subjects repeat L, cut it, put it at the end, put a
+    failing occurrence before a matching one, and R ends with '$' or is empty;
+    the interpreter (the kernel's algorithm) equals the oracle (std::regex_search)."""
+    rng = np.random.default_rng(44)
+    lits = ["/svc%d/v" % i for i in range(40)] + ["/api/w%d/" % i for i in range(40)] + \
+           ["abab%d" % i for i in range(20)] + ["aaaa", "aaab", "xyzw", "/a/b/c/d"]
+    ress = ["", "[0-9]+/(users|items)/[0-9]", "x?$", "[a-c]*z", "(ab)+", "\\.json$", "[^/]+/.*"]
+    pats = sorted({re_escape_lit(l) + str(rng.choice(ress)) for l in lits})
+    rules = [L.PortRuleHTTP(Path=p) for p in pats]
+    prog = HttpProgram(L.RuleSet.compile_http(rules, dialect=RE2).program())
+    assert prog.fields[1][9] != 0xFFFFFFFF
+    subs = []
+    tails = ["", "12/users/7", "x", "zz", "ab", "abab", ".json", "q/r", "/", "9/items/0x"]
+    for _ in range(3000):
+        l1, l2 = str(rng.choice(lits)), str(rng.choice(lits))
+        k = int(rng.integers(0, 6))
+        if k == 0:
+            s = l1 + str(rng.choice(tails))
+        elif k == 1:
+            s = l1[:-1] + str(rng.choice(tails))  # cut literal
+        elif k == 2:
+            s = l2 + "-" + l1 + str(rng.choice(tails))  # second occurrence decides
+        elif k == 3:
+            s = l1 + l1 + str(rng.choice(tails))  # overlapping / repeated
+        elif k == 4:
+            s = str(rng.choice(tails)) + l1  # literal at the end
+        else:
+            s = l1[:2] + l1 + str(rng.choice(tails))
+        subs.append(s)
+    arena, offs = L.pack_http([L.HTTPRequest("GET", s) for s in subs])
+    got = prog.eval(arena, offs)
+    exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
+    bad = np.nonzero(got != exp)[0]
+    assert len(bad) == 0, [(subs[i], int(exp[i]), int(got[i])) for i in bad[:10]]
+    assert (exp >= 0).sum() > 600 and (exp == -1).sum() > 100
+
+
+def re_escape_lit(s):
+    return "".join("\\" + c if c in ".+*?()[]{}|^$\\" else c for c in s)

@@ -8,3 +8,6 @@ step() { local name=$1 secs=$2; shift 2; echo "== $name: $*" >> $OUT/steps.log
 step bench_re2 400 python -u bench.py --dialect re2 --steps 5 --warmup 1 --no-cpu-baseline --no-e2e --no-parity || exit $?
 L7M_LIB=variants/prof.so step prof_re2 400 python -u bench.py --dialect re2 --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-parity --requests 16000000 || exit $?
 L7M_LIB=variants/prof.so step prof_default 400 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --no-parity --no-batcher --requests 16000000 || exit $?
+step batcher 300 ./cilium_amd/batcher_bench 2 1000000 3 0 8 16 || exit $?
+step batcher_eager 300 ./cilium_amd/batcher_bench 2 1000000 3 1 8 16 || exit $?
+step bench_default 400 python -u bench.py --steps 10 --no-cpu-baseline --no-batcher --no-e2e || exit $?
