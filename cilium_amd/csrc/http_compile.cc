@@ -184,7 +184,7 @@ void plan_alit(const std::vector<re::Ast>& asts, const std::vector<uint32_t>& si
       ++freq[g];
     }
   uint32_t buckets = 64;
-  while (buckets < cand.size()) buckets <<= 1;
+  while (buckets < 2 * cand.size()) buckets <<= 1;  // quarter-full: every pattern finds a bucket
   if (16ull * buckets > kAlitMaxLdsBytes) buckets = kAlitMaxLdsBytes / 16;
   out->tab.assign(4ull * buckets, 0u);
   std::map<std::string, uint32_t> rid;

@@ -685,6 +685,7 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
     if (s + ln > pos + len) return;
     const uint32_t* L = base + ap.x;
     bool eq = true;
+#ifndef L7M_DIAG_NOCMP
     for (uint32_t i = 0; eq && i < ln; i += 4) {
       const uint32_t lw = L[i >> 2];
       const uint32_t sw = src.word_u(s + i);
@@ -692,12 +693,18 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
       const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
       eq = ((lw ^ sw) & m) == 0;
     }
+#endif
     if (!eq) return;
+#ifndef L7M_DIAG_NORESID
     if (ap.w != kNone) {
       const uint32_t rc = walk_dfa<false, false>(c, fd.resid_dfa, src, s + ln, pos + len - (s + ln));
       if (!code_has<false>(c, fd.resid_dfa, rc, ap.w)) return;
     }
+#endif
     codes.orbits(ap.z >> 8, 1u << (ap.z & 31u));
+#ifdef L7M_DIAG_NOTOUCH
+    return;
+#endif
     // the pattern's candidate entry is read by verification: start its L2
     // round trip now (as the packed walks' touch does)
     const DfaDesc& gd = c.dds[ap.z >> 8];
@@ -706,55 +713,45 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
       asm volatile("" ::"v"(t));
     }
   };
-  // The probe loop only collects hits -- (pattern, position) packed in one
-  // word -- into kAlitSlots registers; the candidates are processed after it,
-  // all lanes on their j-th candidate together, from ONE call site.
-  // (Processing each hit inside the loop ran the compare + residual walk once
-  // per word for the whole wave whenever any lane had a hit there.)  A lane
-  // whose slots fill up stops probing there; after its candidates are done it
-  // resumes at that position (outer loop).
-  constexpr uint32_t kAlitSlots = 4;
-  uint32_t from = pos;  // next position to probe
-  while (__any(from < end)) {
-    uint32_t cs[kAlitSlots], nc = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kAlitSlots; ++i) cs[i] = 0;
-    auto push = [&](bool hit, uint32_t pid, uint32_t q) {
-#pragma unroll
-      for (uint32_t i = 0; i < kAlitSlots; ++i) cs[i] = hit && nc == i ? (pid << 16 | (q - pos)) : cs[i];
-      nc += hit ? 1u : 0u;
-    };
-    uint32_t stop = end;  // first position not probed in this round
-    auto probe = [&](uint32_t g, uint32_t q) {
-      const bool on = q >= from && q < stop;
-      const u32x4 e = tab[on ? gram_bucket(g) & am : 0u];
-      const bool h0 = on && e.y && e.x == g, h1 = on && e.w && e.z == g;
-      if (nc + (h0 ? 1u : 0u) + (h1 ? 1u : 0u) > kAlitSlots) {  // no room: resume here next round
-        stop = q;
-        return;
-      }
-      push(h0, e.y - 1, q);
-      push(h1, e.w - 1, q);
-    };
+  // Windows of 32 positions: the probes of a window only set hit bits (two
+  // per position: the bucket's two entries) -- no candidate work inside the
+  // probe loop, whose iterations differ per lane --; then each hit re-reads
+  // its bucket and runs the compare / residual walk from one call site.
+  // (Processing hits inside the probe loop ran the candidate code once per
+  // word for the whole wave whenever any lane had a hit there.)
+  for (uint32_t base = pos & ~3u; base < end; base += 32) {
+    uint64_t hm = 0;
     if constexpr (Src::kLds) {
-      uint32_t q = from & ~3u;
-      uint32_t w0 = src.word(q >> 2);
-      for (; q < stop; q += 4) {
-        const uint32_t w1 = src.word((q >> 2) + 1);
+      uint32_t w0 = src.word(base >> 2);
+      for (uint32_t i = 0; i < 8 && base + 4 * i < end; ++i) {
+        const uint32_t w1 = src.word((base >> 2) + i + 1);
 #pragma unroll
-        for (uint32_t sft = 0; sft < 4; ++sft) probe(__builtin_amdgcn_alignbyte(w1, w0, sft), q + sft);
+        for (uint32_t sft = 0; sft < 4; ++sft) {
+          const uint32_t q = base + 4 * i + sft, g = __builtin_amdgcn_alignbyte(w1, w0, sft);
+          const bool on = q >= pos && q < end;
+          const u32x4 e = tab[on ? gram_bucket(g) & am : 0u];
+          const uint32_t h = (on && e.y && e.x == g ? 1u : 0u) | (on && e.w && e.z == g ? 2u : 0u);
+          hm |= static_cast<uint64_t>(h) << (2 * (4 * i + sft));
+        }
         w0 = w1;
       }
     } else {
-      for (uint32_t q = from; q < stop; ++q) probe(src.word_u(q), q);
+      for (uint32_t i = 0; i < 32 && base + i < end; ++i) {
+        const uint32_t q = base + i;
+        if (q < pos) continue;
+        const uint32_t g = src.word_u(q);
+        const u32x4 e = tab[gram_bucket(g) & am];
+        const uint32_t h = (e.y && e.x == g ? 1u : 0u) | (e.w && e.z == g ? 2u : 0u);
+        hm |= static_cast<uint64_t>(h) << (2 * i);
+      }
     }
-    for (uint32_t j = 0; j < nc; ++j) {
-      uint32_t cw = cs[0];
-#pragma unroll
-      for (uint32_t i = 1; i < kAlitSlots; ++i) cw = j == i ? cs[i] : cw;
-      candidate(cw >> 16, pos + (cw & 0xffffu));
+    while (hm) {
+      const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(hm));
+      hm &= hm - 1;
+      const uint32_t q = base + (j >> 1), g = src.word_u(q);
+      const u32x4 e = tab[gram_bucket(g) & am];
+      candidate(((j & 1u) ? e.w : e.y) - 1, q);
     }
-    from = stop;
   }
 }
 

@@ -195,7 +195,11 @@ constexpr uint32_t kAlitExtraLdsBytes = 32u << 10; // descriptors + literals bey
 // cannot match any of the group's patterns.
 constexpr uint32_t kGramMinGroups = 1;      // fields with fewer search groups walk them all
 constexpr uint32_t kGramMaxGroups = 64;
-__host__ __device__ inline uint32_t gram_bucket(uint32_t gram) { return (gram * 0x9e3779b1u) >> 16; }
+// (full-rate VALU only: a 24-bit multiply, no 32-bit one, which is quarter rate)
+__host__ __device__ inline uint32_t gram_bucket(uint32_t gram) {
+  const uint32_t x = gram ^ (gram >> 15);
+  return ((x & 0xffffffu) * 0x9e3779u) >> 10;
+}
 
 // Check record (u32 words, in the check-record pool; lists are sorted by rid):
 //   [0] rule id   [1] n_matchers | port entry << 8 | (has_remote_set << 31)

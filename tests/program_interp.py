@@ -42,6 +42,12 @@ DFA_SEARCH = 1  # program.h kDfaSearch
 DFA_ALIT = 2    # program.h kDfaAlit
 
 
+def gram_bucket(g):
+    """program.h gram_bucket."""
+    x = g ^ (g >> 15)
+    return (((x & 0xFFFFFF) * 0x9E3779) & 0xFFFFFFFF) >> 10
+
+
 def name_hash(data: bytes) -> int:
     """program.h name_hash_step / name_hash_final."""
     M = 0xFFFFFFFF
@@ -99,7 +105,7 @@ class HttpProgram:
         tab, amask, pats, rdfa = fd[9], fd[10], fd[11], fd[12]
         for q in range(len(data) - 3):
             g = int.from_bytes(data[q:q + 4], "little")
-            b = tab + 4 * ((((g * 0x9E3779B1) & 0xFFFFFFFF) >> 16) & amask)
+            b = tab + 4 * (gram_bucket(g) & amask)
             e = self.img[b:b + 4]
             for eg, ep in ((e[0], e[1]), (e[2], e[3])):
                 if not ep or eg != g:
@@ -126,7 +132,7 @@ class HttpProgram:
         m = always
         for i in range(len(data) - 3):
             g = int.from_bytes(data[i:i + 4], "little")
-            b = tab + 4 * ((((g * 0x9E3779B1) & 0xFFFFFFFF) >> 16) & gmask)
+            b = tab + 4 * (gram_bucket(g) & gmask)
             e = self.img[b:b + 4]
             if e[0] == g:
                 m |= e[1]
