@@ -143,7 +143,7 @@ struct AlitField {
   bool on = false;
   uint32_t first_group = 0;            // field group index of the first kDfaAlit group
   std::vector<uint32_t> tab;           // buckets x {gram, pattern + 1, gram, pattern + 1}
-  std::vector<uint32_t> pats;          // field pattern ids in alit order (AlitPat index)
+  std::vector<uint32_t> pats;          // field pattern ids in alit order (AlitRec order)
   std::vector<std::string> lit;        // per alit pattern: L
   std::vector<uint32_t> k;             // per alit pattern: offset of its table gram in L
   std::vector<uint32_t> resid;         // per alit pattern: residual id, kNone = empty
@@ -1041,22 +1041,17 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
 
   // literal-anchored patterns' descriptors and literals, last: in LDS when they fit
   // (else program memory)
-  std::vector<std::vector<uint32_t>> alit_lit_off(nf);
+  std::vector<uint64_t> alit_words(nf, 0);  // AlitRecs (header + literal granules)
+  for (uint32_t f = 0; f < nf; ++f)
+    for (const auto& L : alit[f].lit) alit_words[f] += 4ull * alit_rec_granules(L.size());
   for (uint32_t f = 0; f < nf; ++f) {
     if (fd[f].alit_tab == kNone) continue;
-    uint64_t words = 4ull * alit[f].pats.size();
-    for (const auto& L : alit[f].lit) words += ((L.size() + 3) / 4 + 1 + 3) & ~3ull;
-    // (read once per candidate, but an L2 round trip each from the program:
-    // they may exceed the table budget by kAlitExtraLdsBytes)
-#ifdef L7M_ALIT_NO_LDS
-    continue;
-#endif
-    if (img + words > budget + kAlitExtraLdsBytes / 4 || 4 * (img + words) + codes_bytes + ctr_bytes +
-                                                                 stage_bytes > kHttpLdsBytes)
-      continue;
+    const uint64_t words = alit_words[f];
+    // (read once per candidate: within the table budget only -- config 2's
+    // 1000 path records in LDS shrink the record stage, 32.8 vs 26 ms)
+    if (img + words > budget) continue;
     fd[f].alit_lds = 1;
-    fd[f].alit_pats = img_take(4ull * alit[f].pats.size());
-    for (const auto& L : alit[f].lit) alit_lit_off[f].push_back(img_take((L.size() + 3) / 4 + 1));
+    fd[f].alit_pats = img_take(words);
   }
   // ---- program layout ----
   HttpHeader h;
@@ -1177,12 +1172,12 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       lw[2 * l + 1] = static_cast<uint32_t>(fp.value.size());
     }
   }
-  // literal-anchored patterns: AlitPat[] and the literals (program memory)
+  // literal-anchored patterns' AlitRecs (program memory, 16-byte aligned)
   // when the LDS image has no room for them
   for (uint32_t f = 0; f < nf; ++f) {
     if (fd[f].alit_tab == kNone || fd[f].alit_lds) continue;
-    fd[f].alit_pats = take(4ull * alit[f].pats.size());
-    for (const auto& L : alit[f].lit) alit_lit_off[f].push_back(take((L.size() + 3) / 4 + 1));  // + a zero word
+    w = (w + 3) & ~uint64_t(3);
+    fd[f].alit_pats = take(alit_words[f]);
   }
   w = (w + 63) & ~uint64_t(63);  // 256-byte aligned image
   h.lds_image_off = take(img);
@@ -1271,17 +1266,26 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   for (uint32_t f = 0; f < nf; ++f) {
     if (fd[f].alit_tab == kNone) continue;
     const AlitField& A = alit[f];
-    std::memcpy(I + fd[f].alit_tab, A.tab.data(), A.tab.size() * 4ull);
+    std::vector<uint32_t> gran(A.pats.size());  // pattern -> its AlitRec's granule
+    uint32_t g = 0;
+    for (size_t i = 0; i < A.pats.size(); ++i) {
+      gran[i] = g;
+      g += alit_rec_granules(A.lit[i].size());
+    }
+    std::vector<uint32_t> tab = A.tab;  // {gram, pattern + 1} -> {gram, granule + 1}
+    for (size_t e = 1; e < tab.size(); e += 2)
+      if (tab[e]) tab[e] = gran[tab[e] - 1] + 1;
+    std::memcpy(I + fd[f].alit_tab, tab.data(), tab.size() * 4ull);
+    uint32_t* base = (fd[f].alit_lds ? I : P) + fd[f].alit_pats;
     for (size_t i = 0; i < A.pats.size(); ++i) {
       const auto loc = fp_loc[f][A.pats[i]];  // (group, local id)
-      AlitPat ap;
-      ap.lit = alit_lit_off[f][i];
-      ap.len_k = static_cast<uint32_t>(A.lit[i].size()) | A.k[i] << 16;
-      ap.code = (dfa_first[f] + loc.first) << 8 | loc.second;
-      ap.resid = A.resid[i];
-      uint32_t* base = fd[f].alit_lds ? I : P;
-      std::memcpy(base + fd[f].alit_pats + 4 * i, &ap, sizeof ap);
-      std::memcpy(reinterpret_cast<uint8_t*>(base + alit_lit_off[f][i]), A.lit[i].data(), A.lit[i].size());
+      AlitRec ar;
+      ar.len_k = static_cast<uint32_t>(A.lit[i].size()) | A.k[i] << 16;
+      ar.code = (dfa_first[f] + loc.first) << 8 | loc.second;
+      ar.resid = A.resid[i];
+      ar.pad = 0;
+      std::memcpy(base + 4 * gran[i], &ar, sizeof ar);
+      std::memcpy(reinterpret_cast<uint8_t*>(base + 4 * gran[i] + 4), A.lit[i].data(), A.lit[i].size());
     }
   }
   std::memcpy(P + h.off_fields, fd.data(), fd.size() * sizeof(FieldDesc));

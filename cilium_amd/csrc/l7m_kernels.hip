@@ -670,46 +670,36 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
   if (len < 4) return;
   const u32x4* tab = reinterpret_cast<const u32x4*>(c.img + fd.alit_tab);
   const uint32_t am = fd.alit_mask, end = pos + len - 3;  // grams start in [pos, end)
-  auto candidate = [&](uint32_t pid, uint32_t q) {
-#ifdef L7M_DIAG_ALIT_NOCAND
-    codes.orbits(fd.dfa_first + fd.ndfa - 1, pid & 1u);
-    return;
-#endif
-    // descriptors and literals in LDS or the program (generic pointer: one
-    // flat read either way)
-    const uint32_t* base = fd.alit_lds ? c.img : c.prog;
-    const u32x4 ap = *reinterpret_cast<const u32x4*>(base + fd.alit_pats + 4u * pid);
-    const uint32_t ln = ap.y & 0xffffu, k = ap.y >> 16;
+  auto candidate = [&](uint32_t rec, uint32_t q) {
+    // the AlitRec in LDS or the program (generic pointer): its header and the
+    // first 16 literal bytes in one 32-byte read
+    const u32x4* rp = reinterpret_cast<const u32x4*>(fd.alit_lds ? c.img : c.prog) + (fd.alit_pats >> 2) + rec;
+    const u32x4 a0 = rp[0], a1 = rp[1];
+    const uint32_t ln = a0.x & 0xffffu, k = a0.x >> 16;
     if (q < pos + k) return;
     const uint32_t s = q - k;  // candidate start (record byte offset)
     if (s + ln > pos + len) return;
-    const uint32_t* L = base + ap.x;
     bool eq = true;
-#ifndef L7M_DIAG_NOCMP
     for (uint32_t i = 0; eq && i < ln; i += 4) {
-      const uint32_t lw = L[i >> 2];
+      const uint32_t j = i >> 2;
+      const uint32_t lw = j == 0 ? a1.x : j == 1 ? a1.y : j == 2 ? a1.z : j == 3 ? a1.w
+                                                                              : reinterpret_cast<const uint32_t*>(rp + 1)[j];
       const uint32_t sw = src.word_u(s + i);
       const uint32_t rem = ln - i;
       const uint32_t m = rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u;
       eq = ((lw ^ sw) & m) == 0;
     }
-#endif
     if (!eq) return;
-#ifndef L7M_DIAG_NORESID
-    if (ap.w != kNone) {
+    if (a0.z != kNone) {
       const uint32_t rc = walk_dfa<false, false>(c, fd.resid_dfa, src, s + ln, pos + len - (s + ln));
-      if (!code_has<false>(c, fd.resid_dfa, rc, ap.w)) return;
+      if (!code_has<false>(c, fd.resid_dfa, rc, a0.z)) return;
     }
-#endif
-    codes.orbits(ap.z >> 8, 1u << (ap.z & 31u));
-#ifdef L7M_DIAG_NOTOUCH
-    return;
-#endif
+    codes.orbits(a0.y >> 8, 1u << (a0.y & 31u));
     // the pattern's candidate entry is read by verification: start its L2
     // round trip now (as the packed walks' touch does)
-    const DfaDesc& gd = c.dds[ap.z >> 8];
+    const DfaDesc& gd = c.dds[a0.y >> 8];
     if (gd.lds_ct == kNone) {
-      uint32_t t = gld(c.prog + gd.ct_off + 16u * (ap.z & 31u));
+      uint32_t t = gld(c.prog + gd.ct_off + 16u * (a0.y & 31u));
       asm volatile("" ::"v"(t));
     }
   };
@@ -1244,8 +1234,10 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
     const u32x4* q = reinterpret_cast<const u32x4*>(e);
     check_entry(q[0], q[1], q[2]);
   };
-  // only DFAs with candidate entries
+  // only DFAs with candidate entries (search programs: only those the record
+  // set a code for -- a handful of dozens)
   uint64_t cm = cand_all;
+  if constexpr (kReg < 0) cm &= codes.masked ? codes.valid : ~0ull;
   for (uint32_t i = 0; masked ? cm != 0 : i < h.n_dfas; ++i) {
     uint32_t d = i;
     if (masked) {
@@ -1256,10 +1248,6 @@ __device__ __forceinline__ int32_t eval_verify(const Ctx& c, const HttpHeader& h
     if (!code) continue;
     const DfaDesc& dd = c.dds[d];
     if (kReg < 0 && dd.kind != kDfaPacked) {  // search / alit: candidates of every matched pattern (entry p)
-#ifdef L7M_DIAG_VERIFY_SKIP
-      best = code;
-      continue;
-#endif
       for (uint32_t m = code; m; m &= m - 1) {
         const uint32_t idx = static_cast<uint32_t>(__builtin_ctz(m));
         const uint32_t mw = dd.lds_ctmask != kNone ? lld(c.img + dd.lds_ctmask + (idx >> 5))

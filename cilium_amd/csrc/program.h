@@ -172,24 +172,27 @@ struct FieldDesc {
   // position q whose gram hits, L is compared at q - k and the residual
   // automaton resid_dfa (one packed DFA of the field's distinct R [\x00-\xff]*)
   // is walked from the end of L.  alit_tab: LDS image word offset of
-  // alit_mask + 1 buckets {gram, pattern + 1, gram, pattern + 1} (0 = empty),
-  // kNone = none; alit_pats: word offset of AlitPat[] -- in the LDS image
-  // when alit_lds (the literals too), else in the program (read once per
-  // candidate).
+  // alit_mask + 1 buckets {gram, rec + 1, gram, rec + 1} (0 = empty; rec =
+  // the pattern's AlitRec in 16-byte granules from alit_pats), kNone = none;
+  // alit_pats: word offset (16-byte aligned) of the AlitRecs -- in the LDS
+  // image when alit_lds, else in the program (read once per candidate).
   uint32_t alit_tab, alit_mask, alit_pats, resid_dfa;
   uint32_t alit_lds;
   uint32_t pad[2];
 };
 static_assert(sizeof(FieldDesc) == 64, "field desc is 16 words");
-struct AlitPat {
-  uint32_t lit;    // word offset of L, LDS image or program as the AlitPat (zero padded + one zero word)
+// One literal-anchored pattern: this 16-byte header, then L's bytes zero
+// padded to whole granules, so a candidate's descriptor and its first 16
+// literal bytes are one 32-byte read (one round trip from the program).
+struct AlitRec {
   uint32_t len_k;  // |L| | k << 16 (offset of the table gram in L)
   uint32_t code;   // kDfaAlit group DFA index << 8 | pattern bit (local id)
   uint32_t resid;  // pattern id of R in resid_dfa, or kNone: R is empty (L decides)
+  uint32_t pad;
 };
+inline uint32_t alit_rec_granules(uint64_t lit_len) { return 1u + static_cast<uint32_t>((lit_len + 15) / 16); }
 constexpr uint32_t kAlitMinPatterns = 8;          // fewer: plain search groups
 constexpr uint32_t kAlitMaxLdsBytes = 32u << 10;   // the bucket table
-constexpr uint32_t kAlitExtraLdsBytes = 32u << 10; // descriptors + literals beyond the table budget
 // Every match of a pattern contains its required literal (regex_re2.cc
 // required_literals), so a value lacking all of a group's chosen 4-byte grams
 // cannot match any of the group's patterns.

@@ -111,10 +111,11 @@ class HttpProgram:
                 if not ep or eg != g:
                     continue
                 words, byts = (self.img, self.img_bytes) if fd[13] else (self.w, self.prog_bytes)  # alit_lds
-                lit, len_k, code, resid = words[pats + 4 * (ep - 1): pats + 4 * ep]
+                r = pats + 4 * (ep - 1)  # AlitRec: header granule, then L's bytes
+                len_k, code, resid, _ = words[r:r + 4]
                 ln, k = len_k & 0xFFFF, len_k >> 16
                 s = q - k
-                if s < 0 or s + ln > len(data) or data[s:s + ln] != byts[4 * lit:4 * lit + ln]:
+                if s < 0 or s + ln > len(data) or data[s:s + ln] != byts[4 * (r + 4):4 * (r + 4) + ln]:
                     continue
                 if resid != KNONE:
                     rc = self.walk(rdfa, data[s + ln:])
