@@ -432,7 +432,11 @@ namespace {
 
 constexpr size_t kLitMinBytes = 16;  // shorter literal values are walked byte by byte
 
-CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const PolicyPlan& plan, const l7m_opts& opts) {
+// no_alit: fields whose literal-anchored scan is turned off (their patterns
+// stay search groups); set by compile_http_plan when a field's bucket table
+// does not fit the LDS budget.  *alit_over receives such a field.
+CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const PolicyPlan& plan, const l7m_opts& opts,
+                                uint64_t no_alit, uint32_t* alit_over) {
   CompileResult res;
   auto fail = [&](int st, const std::string& m) {
     res.status = st;
@@ -579,7 +583,8 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       // decides them (gram probe, literal compare, shared residual automaton)
       {
         std::vector<uint32_t> rest;
-        plan_alit(asts, sidx, &alit[f], &rest);
+        if (f < 64 && (no_alit >> f & 1)) rest = sidx;
+        else plan_alit(asts, sidx, &alit[f], &rest);
         sidx = std::move(rest);
       }
       // patterns without a 4-byte required literal ("always" walked) are
@@ -864,6 +869,8 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     fd[f].alit_tab = fd[f].alit_pats = kNone;
     fd[f].alit_mask = 0;
     fd[f].alit_lds = 0;
+    fd[f].alit_granules = 0;
+    fd[f].pad = 0;
     fd[f].resid_dfa = resid_dfa[f];
   }
   std::vector<Span> rremote(n);
@@ -927,9 +934,14 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   // value byte; their groups have no automaton, so it must be resident)
   for (uint32_t f = 0; f < nf; ++f) {
     if (!alit[f].on) continue;
-    if (img + alit[f].tab.size() > budget)
+    if (img + alit[f].tab.size() > budget) {
+      // not resident: the caller compiles again with this field's patterns
+      // as plain search groups (a policy that compiled before the alit scan
+      // existed still compiles)
+      *alit_over = f;
       return fail(L7M_ETOOBIG, field_names[f] + ": the literal-anchored pattern table needs " +
                                    std::to_string(4 * alit[f].tab.size()) + " bytes of LDS");
+    }
     fd[f].alit_tab = img_take(alit[f].tab.size());
     fd[f].alit_mask = static_cast<uint32_t>(alit[f].tab.size() / 4 - 1);
   }
@@ -1272,6 +1284,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       gran[i] = g;
       g += alit_rec_granules(A.lit[i].size());
     }
+    fd[f].alit_granules = g;
     std::vector<uint32_t> tab = A.tab;  // {gram, pattern + 1} -> {gram, granule + 1}
     for (size_t e = 1; e < tab.size(); e += 2)
       if (tab[e]) tab[e] = gran[tab[e] - 1] + 1;
@@ -1334,6 +1347,19 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   return res;
 }
 
+// compile_http_core, and again without the literal-anchored scan of each
+// field whose bucket table did not fit the LDS budget (at most once per field).
+CompileResult compile_http_alit_fallback(const l7m_http_rule* rules, size_t n, const PolicyPlan& plan,
+                                         const l7m_opts& opts) {
+  uint64_t no_alit = 0;
+  for (;;) {
+    uint32_t over = kNone;
+    CompileResult r = compile_http_core(rules, n, plan, opts, no_alit, &over);
+    if (r.status != L7M_ETOOBIG || over == kNone || over >= 64 || (no_alit >> over & 1)) return r;
+    no_alit |= 1ull << over;
+  }
+}
+
 }  // namespace
 
 CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts& opts) {
@@ -1346,7 +1372,7 @@ CompileResult compile_http(const l7m_http_rule* rules, size_t n, const l7m_opts&
   plan.names = {""};
   plan.origin.resize(n);
   for (size_t i = 0; i < n; ++i) plan.origin[i] = {0, 1, 0, 0, static_cast<int32_t>(i), 0};
-  CompileResult r = compile_http_core(rules, n, plan, opts);
+  CompileResult r = compile_http_alit_fallback(rules, n, plan, opts);
   r.names = std::move(plan.names);
   r.origin = std::move(plan.origin);
   return r;
@@ -1436,7 +1462,7 @@ CompileResult compile_http_policies(const l7m_network_policy* pols, size_t npol,
     flat[i].remote_ids = flat_remotes[i].data();
     flat[i].n_remote_ids = static_cast<uint32_t>(flat_remotes[i].size());
   }
-  CompileResult r = compile_http_core(flat.data(), flat.size(), plan, opts);
+  CompileResult r = compile_http_alit_fallback(flat.data(), flat.size(), plan, opts);
   r.names = std::move(plan.names);
   r.origin = std::move(plan.origin);
   return r;

@@ -410,7 +410,11 @@ struct l7m_batcher {
       // first request -- or as soon as every caller inside l7m_batcher_eval that
       // is not already waiting on an evaluated batch is in this one: nobody is
       // left to join it, so waiting out the deadline would only add latency.
-      const int64_t free_callers = static_cast<int64_t>(callers.load()) - in_closed.load();
+      // A hint, not a snapshot: in_closed is read before callers, so a batch
+      // closed or a caller arriving between the two loads makes the estimate
+      // larger, i.e. errs toward waiting.
+      const int64_t closed_now = in_closed.load();
+      const int64_t free_callers = static_cast<int64_t>(callers.load()) - closed_now;
       if (!eager && !stop.load() && cnt0 < max_batch && !b->want_close.load() && static_cast<int64_t>(cnt0) < free_callers &&
           (first == 0 || now_ns() - first < static_cast<int64_t>(max_delay_us) * 1000)) {
         cpu_relax();

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <cstring>
+#include <map>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -29,23 +31,43 @@ inline hipError_t set_lds_attr_once(const void* fn, uint32_t bytes) {
   return e;
 }
 
-// Stream-ordered scratch (hipMallocAsync: the slow pass's executor stacks,
-// the search programs' code columns) comes from the device's default pool;
-// keep its memory mapped between launches instead of returning it at every
-// synchronisation (release threshold 0 by default), once per device.
-inline void keep_stream_pool() {
+// Stream-ordered scratch (the slow pass's executor stacks, the search
+// programs' code columns) comes from a PRIVATE memory pool per device, so
+// the embedding process's default pool (its own hipMallocAsync behaviour) is
+// left alone.  The private pool keeps up to 2 GiB mapped between
+// launches instead of returning it at every synchronisation.  Falls back to
+// the default pool (hipMallocAsync) if the runtime refuses to create one.
+// Free with hipFreeAsync on the base pointer.
+inline hipError_t scratch_alloc_async(void** p, size_t bytes, hipStream_t stream) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
   static std::mutex mu;
-  static std::set<int> done;
-  std::lock_guard<std::mutex> g(mu);
-  if (done.count(dev)) return;
+  static std::map<int, hipMemPool_t> pools;
   hipMemPool_t pool = nullptr;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
-    uint64_t keep = 4ull << 30;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = pools.find(dev);
+    if (it == pools.end()) {
+      hipMemPoolProps props;
+      std::memset(&props, 0, sizeof props);
+      props.allocType = hipMemAllocationTypePinned;
+      props.handleTypes = hipMemHandleTypeNone;
+      props.location.type = hipMemLocationTypeDevice;
+      props.location.id = dev;
+      if (hipMemPoolCreate(&pool, &props) == hipSuccess && pool) {
+        uint64_t keep = 2ull << 30;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      } else {
+        pool = nullptr;
+        (void)hipGetLastError();
+      }
+      pools[dev] = pool;  // nullptr: use the default pool
+    } else {
+      pool = it->second;
+    }
   }
-  done.insert(dev);
+  return pool ? hipMallocFromPoolAsync(p, bytes, pool, stream) : hipMallocAsync(p, bytes, stream);
 }
 
 // LDS bytes of one HTTP workgroup with `stage` bytes of records per wave, and

@@ -670,7 +670,13 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
   if (len < 4) return;
   const u32x4* tab = reinterpret_cast<const u32x4*>(c.img + fd.alit_tab);
   const uint32_t am = fd.alit_mask, end = pos + len - 3;  // grams start in [pos, end)
+  const uint32_t ngran = fd.alit_granules;
   auto candidate = [&](uint32_t rec, uint32_t q) {
+    // rec comes from a bucket entry whose hit bit required it non-zero, so it
+    // is a compiled AlitRec granule; the bound keeps any other value (an
+    // ablated or corrupted scan, r5g's `skip` variant) from forming a pointer
+    // outside the records
+    if (rec >= ngran) return;
     // the AlitRec in LDS or the program (generic pointer): its header and the
     // first 16 literal bytes in one 32-byte read
     const u32x4* rp = reinterpret_cast<const u32x4*>(fd.alit_lds ? c.img : c.prog) + (fd.alit_pats >> 2) + rec;
@@ -1755,7 +1761,7 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
     // thread (n_dfas words each)
     uint32_t* scratch = nullptr;
     const size_t bytes = static_cast<size_t>(h.n_dfas ? h.n_dfas : 1) * grid.x * kBlock * 4u;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&scratch), bytes, stream);
+    hipError_t e = scratch_alloc_async(reinterpret_cast<void**>(&scratch), bytes, stream);
     if (e != hipSuccess) return e;
     if (mode == kNoHits) e = launch_one<kNoHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts,
                                                      hits, stage, scratch);
@@ -1783,16 +1789,18 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
   const uint64_t w1 = static_cast<uint64_t>(num_cus > 0 ? num_cus : 256) * kSlowWavesPerCu;
   const uint32_t blocks1 = static_cast<uint32_t>(waves < w1 ? waves : w1);
   const uint32_t blocks2 = static_cast<uint32_t>(waves < kSlowBlocks2 ? waves : kSlowBlocks2);
+  void* buf = nullptr;  // the one stream-ordered allocation of the slow pass (freed by its base)
   if (h.n_slow) {
-    void* buf = nullptr;
     const size_t v1 = static_cast<size_t>(blocks1) * kSlowBlock * kVmScratchWords * 4u;
     const size_t v2 = static_cast<size_t>(blocks2) * kSlowBlock * kVmScratchWords2 * 4u;
-    keep_stream_pool();
-    hipError_t e = hipMallocAsync(&buf, 512 + 2 * qbytes + v1 + v2, stream);
+    hipError_t e = scratch_alloc_async(&buf, 512 + 2 * qbytes + v1 + v2, stream);
     if (e == hipSuccess) e = hipMemsetAsync(buf, 0, 512, stream);
     if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(buf) + 512, 0, 4, stream);
     if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(buf) + 512 + qbytes, 0, 4, stream);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {
+      if (buf) (void)hipFreeAsync(buf, stream);
+      return e;
+    }
     work = static_cast<uint32_t*>(buf);
     slowq = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 512);
     slowq2 = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 512 + qbytes);
@@ -1834,7 +1842,7 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
       }
     }
 #undef L7M_SLOW
-    const hipError_t e2 = hipFreeAsync(slowq, stream);
+    const hipError_t e2 = hipFreeAsync(buf, stream);
     if (e == hipSuccess) e = e2;
   }
   return e;

@@ -178,7 +178,8 @@ struct FieldDesc {
   // image when alit_lds, else in the program (read once per candidate).
   uint32_t alit_tab, alit_mask, alit_pats, resid_dfa;
   uint32_t alit_lds;
-  uint32_t pad[2];
+  uint32_t alit_granules;  // 16-byte granules of the AlitRecs: every rec of a table entry is below it
+  uint32_t pad;
 };
 static_assert(sizeof(FieldDesc) == 64, "field desc is 16 words");
 // One literal-anchored pattern: this 16-byte header, then L's bytes zero

@@ -65,7 +65,8 @@ constexpr int kVmNoMatch = 0, kVmMatched = 1, kVmLimit = -1, kVmDeep = -2;
 // 1 MiB (kVmScratchWords2) and 2^25 steps.  Only past those is its verdict
 // L7M_VERDICT_UNSUPPORTED.  Why 1 MiB: libstdc++'s recursive executor (the
 // reference engine) keeps one native frame per NFA state on the current path,
-// which measured (GCC 11, -O0 / -O2, tests/cpp/regex_stack_probe.cc) >= 11
+// which measured (GCC 11: oracle/l7oracle.cc run_on_measured_stack, checked by
+// tests/test_slow_tiers_cpu.py) >= 11
 // bytes of native stack per byte of this explicit stack on every pattern
 // family probed; a subject that needs more than 1 MiB here needs > 8 MiB of
 // native stack there -- past the 8 MiB default thread stack of an Envoy

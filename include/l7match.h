@@ -390,7 +390,12 @@ int l7m_multi_eval(l7m_multi* m, const l7m_ruleset* rs, const uint8_t* arena, si
 /* Device-resident shards (HBM): shard k lives on device k of the set (its
  * pointers are device pointers there; rec_offsets relative to its arena).
  * Synchronous: returns after every device's kernels and the counter
- * all-reduce; rule_hits (host, n_rules + 2) accumulates the job's sum. */
+ * all-reduce; rule_hits (host, n_rules + 2) accumulates the job's sum.
+ * The set evaluates on its own (non-blocking) streams and takes no caller
+ * stream: the shards' contents must be complete on their devices when this
+ * is called (synchronise the stream or device that produced them first, e.g.
+ * hipStreamSynchronize / torch.cuda.synchronize()); nothing orders the
+ * kernels after a producer still in flight. */
 typedef struct {
   const void* arena;
   size_t arena_bytes;

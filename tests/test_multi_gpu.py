@@ -66,6 +66,7 @@ def test_device_set_kafka_map_and_device_shards(gpu):
         keep.append(dv)
         shards.append((da, a1 - a0, do, hi - lo, dv, di))
     h = np.zeros(rs.n_counters, dtype=np.uint64)
+    torch.cuda.synchronize()  # the set's own streams are not ordered after torch's (include/l7match.h)
     ds.eval_device(rs, shards, h)
     got = torch.cat(keep).cpu().numpy()
     assert np.array_equal(got, exp)

@@ -217,3 +217,21 @@ def test_literal_anchored_patterns_exact():
 
 def re_escape_lit(s):
     return "".join("\\" + c if c in ".+*?()[]{}|^$\\" else c for c in s)
+
+
+def test_alit_table_over_lds_budget_falls_back_to_search_groups():
+    """a literal-anchored bucket table that does not fit the LDS
+    budget used to fail the compile (L7M_ETOOBIG).  The field's patterns now
+    fall back to search groups: every budget compiles, the small ones without
+    the alit scan, and every program equals the oracle."""
+    rules = W.rules(2, n_rules=300)
+    arena, offs = W.requests(2, 0, 1200, n_rules=300)
+    exp = HttpOracle(rules, dialect=RE2).eval(arena, offs, threads=8)
+    seen = set()
+    for budget in (1, 2048, 8192, 16384, 49152):
+        prog = HttpProgram(L.RuleSet.compile_http(rules, dialect=RE2, lds_budget_bytes=budget).program())
+        seen.add(prog.fields[1][9] != 0xFFFFFFFF)
+        got = prog.eval(arena, offs)
+        bad = np.nonzero(got != exp)[0]
+        assert len(bad) == 0, (budget, [(int(i), int(exp[i]), int(got[i])) for i in bad[:10]])
+    assert seen == {True, False}
