@@ -507,6 +507,15 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   // slow-path programs (regex_vm.h) of the patterns whose automata are
   // supersets (back-references, oversized look-ahead): [field][pattern]
   std::vector<std::vector<std::vector<uint32_t>>> slow_vm(nf);
+  // back-references whose capture is forced (regex_ecma.h DcapForm): decided
+  // in the first pass; [field][pattern] -> dcap id, kNone otherwise
+  std::vector<std::vector<uint32_t>> dcap_of(nf);
+  struct DcapOut {
+    uint32_t field;
+    re::DcapForm form;
+    PackedDfa rpk;  // R's full-match automaton (unless form.r_empty)
+  };
+  std::vector<DcapOut> dcaps;
   // field pattern -> (group, local id)
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> fp_loc(nf);
   std::vector<GramFilter> gram(nf);  // RE2 dialect: per field, which search groups a value may need
@@ -516,6 +525,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     std::vector<re::Ast> asts(fpats[f].size());
     std::vector<const re::Ast*> ptrs;
     slow_vm[f].resize(fpats[f].size());
+    dcap_of[f].assign(fpats[f].size(), kNone);
     for (size_t p = 0; p < fpats[f].size(); ++p) {
       const auto& fp = fpats[f][p];
       if (fp.kind == MatchKind::Regex && re2) {
@@ -554,6 +564,23 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
           if (re::build_dfa({&asts[p]}, ll, &probe) != re::Status::Ok) {
             asts[p] = re::drop_lookahead(asts[p]);
             exact = false;
+          }
+        }
+        re::DcapForm form;
+        if (!exact && dcaps.size() < kMaxDcap && re::analyze_dcap(full, &form)) {
+          // a forced capture: the superset automaton plus byte compares in
+          // the first pass decide it exactly (no slow path)
+          DcapOut dc;
+          dc.field = f;
+          dc.form = std::move(form);
+          if (!dc.form.r_empty) {
+            std::vector<const re::Ast*> rp{&dc.form.r};
+            if (build_field_dfa(rp, FieldDfaLimits(), &dc.rpk) != re::Status::Ok) dc.field = kNone;
+          }
+          if (dc.field != kNone) {
+            dcap_of[f][p] = static_cast<uint32_t>(dcaps.size());
+            dcaps.push_back(std::move(dc));
+            exact = true;
           }
         }
         if (!exact) {
@@ -763,6 +790,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
         }
         const uint32_t kind = m.kind == MatchKind::Present ? 1u : 0u;
         cr.push_back(m.field | (kind << 8) | (dfa << 9));
+        if (m.fpat != kNone && dcap_of[m.field][m.fpat] != kNone) pat |= (dcap_of[m.field][m.fpat] + 1) << kDcapShift;
         cr.push_back(pat);
       }
     }
@@ -786,6 +814,13 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     if (alit[f].on && alit[f].n_resid) {
       resid_dfa[f] = static_cast<uint32_t>(all.size());
       all.push_back({&alit[f].resid_pk, f, alit[f].n_resid, nullptr});
+    }
+  // forced-capture patterns' R automata (after those)
+  std::vector<uint32_t> dcap_rdfa(dcaps.size(), kNone);
+  for (size_t k = 0; k < dcaps.size(); ++k)
+    if (!dcaps[k].form.r_empty) {
+      dcap_rdfa[k] = static_cast<uint32_t>(all.size());
+      all.push_back({&dcaps[k].rpk, dcaps[k].field, 1, nullptr});
     }
   const uint32_t ndt = static_cast<uint32_t>(all.size());
 
@@ -870,7 +905,9 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     fd[f].alit_mask = 0;
     fd[f].alit_lds = 0;
     fd[f].alit_granules = 0;
-    fd[f].pad = 0;
+    fd[f].dcap_mask = 0;
+    for (size_t k = 0; k < dcaps.size(); ++k)
+      if (dcaps[k].field == f) fd[f].dcap_mask |= 1u << k;
     fd[f].resid_dfa = resid_dfa[f];
   }
   std::vector<Span> rremote(n);
@@ -904,6 +941,16 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   const uint32_t lds_dfas = img_take(static_cast<uint64_t>(ndt) * sizeof(DfaDesc) / 4);
   const uint32_t lds_fields = img_take(static_cast<uint64_t>(nf) * sizeof(FieldDesc) / 4);
   const uint32_t lds_name_field = img_take(name_field.size());
+  // forced-capture specs and their literals (read by every walk of their field)
+  uint32_t lds_dcap = kNone;
+  std::vector<uint32_t> dcap_p1(dcaps.size()), dcap_l2(dcaps.size());
+  if (!dcaps.empty()) {
+    lds_dcap = img_take(16ull * dcaps.size());
+    for (size_t k = 0; k < dcaps.size(); ++k) {
+      dcap_p1[k] = img_take((dcaps[k].form.p1.size() + 3) / 4);
+      dcap_l2[k] = img_take((dcaps[k].form.l2.size() + 3) / 4);
+    }
+  }
   {
     const uint64_t fixed = 4 * img + codes_bytes + ctr_bytes + stage_bytes;
     if (fixed > kHttpLdsBytes)
@@ -1112,7 +1159,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     h.pres_fields_hi = static_cast<uint32_t>(pm >> 32);
   }
   h.n_policies = plan.n_policies;
-  h.pair_pa = 0;  // (unused; the paired walk measured slower, profiles/r03/ab_round3.md)
+  h.lds_dcap = lds_dcap;
   // slow path: Span[n_rules] into the pool of (field, program offset) pairs,
   // then the programs
   h.off_slow = kNone;
@@ -1273,6 +1320,22 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   }
   std::memcpy(P + h.off_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
   std::memcpy(I + lds_dfas, dd.data(), dd.size() * sizeof(DfaDesc));
+  for (size_t k = 0; k < dcaps.size(); ++k) {
+    const re::DcapForm& F = dcaps[k].form;
+    DcapSpec sp;
+    std::memset(&sp, 0, sizeof sp);
+    sp.lens = static_cast<uint32_t>(F.p1.size()) | static_cast<uint32_t>(F.l2.size()) << 16;
+    sp.min = static_cast<uint32_t>(F.min);
+    sp.max = F.max < 0 ? kNone : static_cast<uint32_t>(F.max);
+    sp.rdfa = dcap_rdfa[k];
+    for (int b = 0; b < 256; ++b)
+      if (F.cls.test(b)) sp.cls[b >> 5] |= 1u << (b & 31);
+    sp.p1 = dcap_p1[k];
+    sp.l2 = dcap_l2[k];
+    std::memcpy(I + lds_dcap + 16 * k, &sp, sizeof sp);
+    std::memcpy(I + dcap_p1[k], F.p1.data(), F.p1.size());
+    std::memcpy(I + dcap_l2[k], F.l2.data(), F.l2.size());
+  }
   for (uint32_t f = 0; f < nf; ++f)
     if (fd[f].gram_tab != kNone) std::memcpy(I + fd[f].gram_tab, gram[f].tab.data(), gram[f].tab.size() * 4ull);
   for (uint32_t f = 0; f < nf; ++f) {

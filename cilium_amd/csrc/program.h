@@ -179,7 +179,7 @@ struct FieldDesc {
   uint32_t alit_tab, alit_mask, alit_pats, resid_dfa;
   uint32_t alit_lds;
   uint32_t alit_granules;  // 16-byte granules of the AlitRecs: every rec of a table entry is below it
-  uint32_t pad;
+  uint32_t dcap_mask;      // DcapSpecs (HttpHeader::lds_dcap) of this field's forced-capture patterns
 };
 static_assert(sizeof(FieldDesc) == 64, "field desc is 16 words");
 // One literal-anchored pattern: this 16-byte header, then L's bytes zero
@@ -268,7 +268,7 @@ struct HttpHeader {
   uint32_t pres_fields_lo; // bit f: field f has a presence-keyed check-record list
   uint32_t pres_fields_hi;
   uint32_t search;         // 1: some value DFA is a kDfaSearch automaton (RE2 dialect)
-  uint32_t pair_pa;        // (unused, 0)
+  uint32_t lds_dcap;       // LDS image word offset of DcapSpec[<= kMaxDcap], or kNone
   uint32_t off_slow;       // Span[n_rules] into the pool: (field, slow program offset) pairs of the
                            // rules with kCrSlow matchers (regex_vm.h), or kNone
   uint32_t n_slow;         // rules with slow-path matchers
@@ -278,6 +278,29 @@ struct HttpHeader {
 // {hash (0 = empty), len, field, image word offset of the zero-padded name}.
 // Replaces the walk of the header-name DFA when it fits kMaxNameTabBytes.
 constexpr uint32_t kMaxNameTabBytes = 8192;
+
+// A back-reference pattern whose capture is forced (regex_ecma.h DcapForm,
+// ECMAScript dialect): decided in the first pass.  The field's walk phase
+// evaluates every DcapSpec of FieldDesc::dcap_mask on the value -- P1 compare,
+// the maximal run of class bytes (length in [min, max]), L2 compare, the
+// run compared with the bytes after L2, R's full-match automaton (value DFA
+// rdfa, pattern 0) over the rest -- and sets bit k of the request's dcap
+// mask when spec k holds.  The pattern keeps its superset automaton in the
+// field's groups; a check-record matcher on it carries (k + 1) << kDcapShift
+// in its pattern word, and verification requires bit k as well.
+constexpr uint32_t kMaxDcap = 32;
+constexpr uint32_t kDcapShift = 24;
+constexpr uint32_t kPatMask = (1u << kDcapShift) - 1u;
+struct DcapSpec {
+  uint32_t lens;      // |P1| | |L2| << 16
+  uint32_t min, max;  // run length bounds (max kNone: unbounded)
+  uint32_t rdfa;      // R's automaton (a value DFA of the program), kNone: R empty (the rest must be empty)
+  uint32_t cls[8];    // class bitmap: byte b in C iff bit b
+  uint32_t p1;        // LDS image word offset of P1's bytes (zero-padded words)
+  uint32_t l2;        // ... of L2's bytes
+  uint32_t pad[2];
+};
+static_assert(sizeof(DcapSpec) == 64, "dcap spec is 16 words");
 static_assert(sizeof(HttpHeader) == 160, "header is 40 words");
 
 // ---------------------------------------------------------------- Kafka --

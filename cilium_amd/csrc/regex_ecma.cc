@@ -19,6 +19,7 @@
 #include "regex_ecma.h"
 
 #include <algorithm>
+#include <functional>
 #include <cstring>
 #include <locale>
 #include <map>
@@ -1430,6 +1431,101 @@ Status build_dfa(const std::vector<const Ast*>& patterns, const DfaLimits& lim, 
   kern.clear();
   kern.shrink_to_fit();
   return finish_dfa(n0, ncls, cls, next, endset, midset, start_id, std::move(sets), lim, with_mid, out);
+}
+
+
+// Back-references whose capture is forced (see regex_ecma.h DcapForm).
+bool analyze_dcap(const Ast& a, DcapForm* out) {
+  if (a.root < 0) return false;
+  // exactly one back-reference, to a group that occurs once
+  int nref = 0, ref = -1;
+  for (const Node& n : a.nodes)
+    if (n.kind == Node::Backref) {
+      ++nref;
+      ref = n.min;
+    }
+  if (nref != 1) return false;
+  // the top-level concatenation, Cat nodes flattened
+  std::vector<int> items;
+  std::vector<int> stack{a.root};
+  std::function<void(int)> flat = [&](int x) {
+    if (a.nodes[x].kind == Node::Cat) {
+      for (int k : a.nodes[x].kids) flat(k);
+    } else {
+      items.push_back(x);
+    }
+  };
+  flat(a.root);
+  int ig = -1, ib = -1;
+  for (size_t i = 0; i < items.size(); ++i) {
+    const Node& n = a.nodes[items[i]];
+    if (n.kind == Node::Group && n.min == ref) ig = static_cast<int>(i);
+    if (n.kind == Node::Backref) ib = static_cast<int>(i);
+  }
+  if (ig < 0 || ib < 0 || ib < ig + 2) return false;  // L2 non-empty: group, >= 1 literal, \k
+  auto single = [&](int x, uint8_t* b) {
+    const Node& n = a.nodes[x];
+    if (n.kind != Node::Set || n.set.count() != 1) return false;
+    for (int c = 0; c < 256; ++c)
+      if (n.set.test(c)) *b = static_cast<uint8_t>(c);
+    return true;
+  };
+  DcapForm f;
+  for (int i = 0; i < ig; ++i) {  // P1: an optional leading '^', then literal bytes
+    if (i == 0 && a.nodes[items[0]].kind == Node::Bol) continue;
+    uint8_t b;
+    if (!single(items[i], &b)) return false;
+    f.p1.push_back(static_cast<char>(b));
+  }
+  // G: C, C*, C+, C{n}, C{n,}, C{n,m} of one byte class C
+  const Node& g = a.nodes[items[ig]];
+  if (g.kids.size() != 1) return false;
+  const Node& gk = a.nodes[g.kids[0]];
+  if (gk.kind == Node::Set) {
+    f.cls = gk.set;
+    f.min = f.max = 1;
+  } else if (gk.kind == Node::Rep && gk.kids.size() == 1 && a.nodes[gk.kids[0]].kind == Node::Set) {
+    f.cls = a.nodes[gk.kids[0]].set;
+    f.min = gk.min;
+    f.max = gk.max;
+  } else {
+    return false;
+  }
+  if (f.cls.none()) return false;
+  for (int i = ig + 1; i < ib; ++i) {  // L2: literal bytes, the first outside C
+    uint8_t b;
+    if (!single(items[i], &b)) return false;
+    if (i == ig + 1 && f.cls.test(b)) return false;
+    f.l2.push_back(static_cast<char>(b));
+  }
+  // R: the rest, regular and context-free at its start (no ^, \b, \B,
+  // look-ahead, groups referenced: the pattern's only reference is \k)
+  Ast r;
+  std::vector<int> rk;
+  for (size_t i = ib + 1; i < items.size(); ++i) {
+    const int x = items[i];
+    std::vector<int> todo{x};
+    while (!todo.empty()) {
+      const Node& n = a.nodes[todo.back()];
+      todo.pop_back();
+      if (n.kind == Node::Bol || n.kind == Node::WordB || n.kind == Node::Look || n.kind == Node::Backref) return false;
+      for (int k : n.kids) todo.push_back(k);
+    }
+    rk.push_back(copy_subtree(a, x, &r));
+  }
+  f.r_empty = rk.empty();
+  if (!f.r_empty) {
+    Node cat;
+    cat.kind = Node::Cat;
+    cat.kids = rk;
+    r.nodes.push_back(cat);
+    r.root = static_cast<int>(r.nodes.size()) - 1;
+    bool exact = true;
+    f.r = lower_for_dfa(r, &exact);
+    if (!exact) return false;
+  }
+  *out = std::move(f);
+  return true;
 }
 
 }  // namespace re

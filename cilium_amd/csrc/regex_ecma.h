@@ -121,6 +121,26 @@ bool split_literal_prefix(const Ast& a, std::string* lit, Ast* resid);
 bool residual_is_empty(const Ast& resid);  // R was empty: L alone decides
 std::string ast_key(const Ast& a);          // structural key (dedupes residuals)
 
+// Back-references whose capture is forced (ECMAScript full match).  A pattern
+//     [^] P1 ( C{n,m} ) L2 \k R
+// -- P1 and L2 literal byte strings, C one byte class, the first byte of L2
+// outside C, k the pattern's only back-reference, R regular with no ^, \b,
+// \B or look-ahead -- matches a value v iff v starts with P1, the maximal run
+// of C bytes after it has a length r in [n, m], L2 follows it, the same r
+// bytes follow L2, and R full-matches the rest: group k cannot end anywhere
+// but at the first byte outside C (L2[0] must follow it), so the capture is
+// that run and no backtracking can choose another.  E.g. /(\w+)/\1(/.*)?
+// (P1 "/", C \w, L2 "/", R (/.*)?).  Such patterns are decided in the first
+// pass by byte compares (program.h DcapSpec) instead of the slow path.
+struct DcapForm {
+  std::string p1, l2;
+  ByteSet cls;
+  int min = 1, max = -1;  // max < 0: unbounded
+  bool r_empty = true;
+  Ast r;                  // R, lowered (groups dissolved); full-match automaton
+};
+bool analyze_dcap(const Ast& full, DcapForm* out);
+
 }  // namespace re
 
 // The slow path's program for a full AST (regex_vm.cc, executed by

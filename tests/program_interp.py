@@ -32,7 +32,7 @@ HDR_FIELDS = ("magic n_rules n_fields n_dfas always_rule allow_no_l7 has_name_df
               "off_name_field off_sets off_cr off_pool off_remotes any_remotes zero_off zero_len "
               "lds_image_off lds_image_words lds_dfas lds_fields lds_name_field total_words lds_name_tab "
               "name_tab_mask single_entry n_policies ent_tab_off lds_ent_tab ent_mask name_len_lo name_len_hi "
-              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search pair_pa off_slow n_slow").split()
+              "cand_dfas_lo cand_dfas_hi pres_fields_lo pres_fields_hi search lds_dcap off_slow n_slow").split()
 DFA_FIELDS = ("table_off es_off latch_off ct_off lds_table lds_es lds_latch lds_ct lds_mask start_base region "
               "start_latch n_slots nsets npats set_base field nstates lds_ctmask ctmask_off start_es8 lit_tab "
               "lds_skip skip_lim kind acc_cmap_off acc_mid_off acc_ncls lds_search lds_mid").split()
@@ -40,6 +40,7 @@ ES_IN_ENTRY = 0xFFFFFFFE  # program.h kLdsEsInEntry
 DFA_WORDS = 32  # sizeof(DfaDesc) / 4
 DFA_SEARCH = 1  # program.h kDfaSearch
 DFA_ALIT = 2    # program.h kDfaAlit
+DCAP_SHIFT, PAT_MASK = 24, (1 << 24) - 1  # program.h kDcapShift / kPatMask
 
 
 def gram_bucket(g):
@@ -80,6 +81,17 @@ class HttpProgram:
             r = self.w[h["off_fields"] + 16 * f + 12]
             if r != KNONE:
                 ndt = max(ndt, r + 1)
+        # forced-capture patterns' R automata follow those (program.h DcapSpec)
+        self.dcaps = []
+        if h["lds_dcap"] != KNONE:
+            dm = 0
+            for f in range(h["n_fields"]):
+                dm |= self.w[h["off_fields"] + 16 * f + 15]
+            for k in range(dm.bit_length()):
+                sp = self.img[h["lds_dcap"] + 16 * k: h["lds_dcap"] + 16 * k + 16]
+                self.dcaps.append(sp)
+                if sp[3] != KNONE:
+                    ndt = max(ndt, sp[3] + 1)
         self.dfas = []
         for k in range(ndt):
             o = h["lds_dfas"] + DFA_WORDS * k  # the kernel reads the LDS copy
@@ -89,7 +101,7 @@ class HttpProgram:
             self.dfas.append(d)
         # program.h FieldDesc (16 words): dfa_first, ndfa, presence off/len,
         # gram_tab, gram_mask, always, search_first, n_search, alit_tab,
-        # alit_mask, alit_pats, resid_dfa, pad
+        # alit_mask, alit_pats, resid_dfa, alit_lds, alit_granules, dcap_mask
         self.fields = [tuple(self.img[h["lds_fields"] + 16 * f: h["lds_fields"] + 16 * f + 16])
                        for f in range(h["n_fields"])]
         self.prog_bytes = self.prog.tobytes()
@@ -122,6 +134,30 @@ class HttpProgram:
                     if not self.code_has(rdfa, rc, resid):
                         continue
                 codes[code >> 8] |= 1 << (code & 31)
+
+    def dcap_holds(self, k, data: bytes):
+        """Forced-capture back-reference pattern k (program.h DcapSpec):
+        P1, the maximal class run (length in [min, max]), L2, the run
+        repeated, then R's automaton on the rest."""
+        sp = self.dcaps[k]
+        l1, l2 = sp[0] & 0xFFFF, sp[0] >> 16
+        mn, mx, rdfa, cls = sp[1], sp[2], sp[3], sp[4:12]
+        p1 = self.img_bytes[4 * sp[12]: 4 * sp[12] + l1]
+        lit2 = self.img_bytes[4 * sp[13]: 4 * sp[13] + l2]
+        if len(data) < l1 + l2 or data[:l1] != p1:
+            return False
+        e = l1
+        while e < len(data) and (cls[data[e] >> 5] >> (data[e] & 31)) & 1:
+            e += 1
+        r = e - l1
+        if r < mn or r > mx or e + l2 + r > len(data):
+            return False
+        if data[e:e + l2] != lit2 or data[e + l2:e + l2 + r] != data[l1:e]:
+            return False
+        t = e + l2 + r
+        if rdfa == KNONE:
+            return t == len(data)
+        return self.code_has(rdfa, self.walk(rdfa, data[t:]), 0)
 
     def gram_select(self, f, data: bytes):
         """RE2-dialect gram filter (program.h FieldDesc::gram_tab): the mask
@@ -334,6 +370,7 @@ class HttpProgram:
             e = (hd >> 8) & ((1 << 22) - 1)
             return e == ex or (h0 and e == e0)
         codes = [0] * h["n_dfas"]
+        dmask = [0]  # forced-capture patterns that hold
         present = 0
         pos = 20 + 4 * nhdr
         fvals = {}
@@ -353,6 +390,11 @@ class HttpProgram:
                 codes[k] = self.walk(k, data)
             if self.fields[f][9] != KNONE:
                 self.alit_scan(f, data, codes)
+            if h["lds_dcap"] != KNONE:
+                m = self.fields[f][15]
+                for k in range(32):
+                    if (m >> k) & 1 and self.dcap_holds(k, data):
+                        dmask[0] |= 1 << k
 
         for f, flag, ln in ((0, L.F_METHOD, mlen), (1, L.F_PATH, plen), (2, L.F_AUTHORITY, alen)):
             if flags & flag:
@@ -401,7 +443,9 @@ class HttpProgram:
                     if not (present >> (a & 0xFF)) & 1:
                         ok = False
                     elif not (a >> 8) & 1:
-                        ok = self.code_has(a >> 9, codes[a >> 9], pat)
+                        dk = pat >> DCAP_SHIFT
+                        ok = self.code_has(a >> 9, codes[a >> 9], pat & PAT_MASK) and \
+                            (dk == 0 or bool((dmask[0] >> (dk - 1)) & 1))
                 if ok and hd & CR_SLOW:  # a superset automaton matched
                     if not slow:
                         min_slow[0] = min(min_slow[0], rid)

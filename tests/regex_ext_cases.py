@@ -74,3 +74,49 @@ def realistic_requests(rng, n):
                                   str(rng.choice(hosts)) or None,
                                   [("x-tenant", "t1")] if rng.random() < 0.5 else []))
     return reqs
+
+
+# Back-references whose capture is forced (regex_ecma.h DcapForm: P1 (C{n,m})
+# L2 \1 R with L2[0] outside C), decided in the first pass by byte compares,
+# beside near-miss forms that keep the slow path (L2[0] inside C, the
+# reference inside a repetition, two references).
+DCAP_P1 = ["", "/", "/api/", "x", "^/"]
+DCAP_G = ["(\\w+)", "([a-c]*)", "(\\d{2,3})", "([^/]+)", "(.)", "([a-z]{1,4})"]
+DCAP_L2 = ["/", "-", "--", "/x", "."]
+DCAP_R = ["", "(/.*)?", "\\.json", "[0-9]*$", "/[a-z]+", "(x|yz)*"]
+
+
+def dcap_rules(rng, n):
+    rules = []
+    for _ in range(n):
+        p1, g, l2, r = (str(rng.choice(x)) for x in (DCAP_P1, DCAP_G, DCAP_L2, DCAP_R))
+        form = rng.random()
+        if form < 0.75:
+            pat = p1 + g + l2 + "\\1" + r
+        elif form < 0.85:
+            pat = p1 + g + l2 + "\\1\\1" + r          # two references: slow path
+        elif form < 0.95:
+            pat = p1 + "(?:" + g + l2 + ")+\\1" + r    # reference after a loop: slow path
+        else:
+            pat = p1 + g + "\\1" + r                   # no separator: slow path
+        rules.append(L.PortRuleHTTP(Path=pat, Method=str(rng.choice(["", "GET", "P[A-Z]+"]))))
+    return rules
+
+
+def dcap_requests(rng, n):
+    """Paths built from the forms' pieces: repeated runs, runs that differ in
+    one byte or in length, missing separators, runs cut by the end."""
+    runs = ["a", "ab", "abc", "users", "12", "123", "1234", "x_1", "", "Zz9", "a.b", "cab"]
+    reqs = []
+    for _ in range(n):
+        p1 = str(rng.choice(["", "/", "/api/", "x", "//"]))
+        r1 = str(rng.choice(runs))
+        k = rng.random()
+        r2 = r1 if k < 0.6 else (r1[:-1] if k < 0.7 else r1 + "a" if k < 0.8 else str(rng.choice(runs)))
+        l2 = str(rng.choice(["/", "-", "--", "/x", ".", ""]))
+        tail = str(rng.choice(["", "/", "/x/y", ".json", "123", "xyz", "x", "/abc", "-"]))
+        path = p1 + r1 + l2 + r2 + tail
+        if rng.random() < 0.05:
+            path = path[: int(rng.integers(0, len(path) + 1))]
+        reqs.append(L.HTTPRequest(str(rng.choice(["GET", "POST", "PUT"])), path))
+    return reqs

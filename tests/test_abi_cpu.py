@@ -20,8 +20,11 @@ def test_c_harness_links_and_fails_without_device(tmp_path):
 
 def test_kernel_code_hash_covers_both_kernel_objects():
     """bench.py keys measured traffic on the device code objects' hash
-    (cilium_amd/codehash.py): the library holds the HTTP and the Kafka gfx950
-    code objects, and the hash is stable and differs from the file hash."""
+    (cilium_amd/codehash.py): the library holds the gfx950 code objects of
+    every device translation unit -- the HTTP launcher (search-dialect and
+    diagnostic instantiations), the Kafka kernels and the four HTTP feature
+    sets (l7m_http_feat.hip) -- and the hash is stable and differs from the
+    file hash."""
     import hashlib
     import struct
     from cilium_amd import l7match as L
@@ -38,6 +41,6 @@ def test_kernel_code_hash_covers_both_kernel_objects():
             n_gfx += b"gfx950" in data[p:p + idlen] and size > 0
             p += idlen
         i = j + 1
-    assert n_gfx == 2
+    assert n_gfx == 6
     k = kernel_md5(L.LIB_PATH)
     assert k == kernel_md5(L.LIB_PATH) and k != hashlib.md5(data).hexdigest()

@@ -115,6 +115,28 @@ def test_word_boundary_lookahead_and_backreference_rules_match_oracle():
         _interp_vs_oracle(rules, arena, offs)
 
 
+def test_forced_capture_backreferences_first_pass_match_oracle():
+    """Back-references whose capture is forced (regex_ecma.h DcapForm, e.g.
+    bench.py --extended's /(\\w+)/\\1(/.*)?) are decided in the first pass by
+    byte compares (program.h DcapSpec) instead of the slow path; near-miss
+    forms keep the slow path.  The program interpreter (the kernel's
+    algorithm) equals std::regex_match on paths built to hit and miss them."""
+    rng = np.random.default_rng(61)
+    n_dcap = n_slow = 0
+    for trial in range(12):
+        rules = X.dcap_rules(rng, int(rng.integers(1, 12)))
+        prog = HttpProgram(L.RuleSet.compile_http(rules).program())
+        n_dcap += len(prog.dcaps)
+        n_slow += prog.h["n_slow"]
+        arena, offs = L.pack_http(X.dcap_requests(rng, 1500))
+        v = _interp_vs_oracle(rules, arena, offs)
+        assert (v >= 0).any()
+    assert n_dcap > 20 and n_slow > 0
+    # the extended rules' /(\\w+)/\\1(/.*)? leaves the slow path
+    prog = HttpProgram(L.RuleSet.compile_http(X.REALISTIC).program())
+    assert len(prog.dcaps) == 1 and prog.h["n_slow"] == 1
+
+
 def test_unknown_dialect_is_rejected():
     with pytest.raises(L.L7Error) as e:
         L.RuleSet.compile_http([L.PortRuleHTTP(Path="/a")], dialect=7)

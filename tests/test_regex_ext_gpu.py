@@ -91,9 +91,25 @@ def test_slow_path_decides_what_the_reference_decides(gpu):
 
 def test_extended_rules_slow_pass_share(gpu):
     """bench.py --extended's workload: config 2 with the extended rules in
-    front.  Most requests are deferred to the slow pass (the back-reference
-    rule's superset automaton matches config-2 paths); no verdict is −3."""
+    front.  The back-reference rule whose superset automaton matches most
+    config-2 paths (/(\\w+)/\\1(/.*)?) is a forced capture decided in the
+    first pass (program.h DcapSpec); no verdict is −3."""
     rules = list(X.REALISTIC) + W.rules(2)
     arena, offs = W.requests(2, 5_000_000, 300_000, n_rules=1000)
     got = _check(rules, arena, offs)
     assert L.VERDICT_UNSUPPORTED not in got.tolist()
+
+
+def test_forced_capture_backreferences(gpu):
+    """Back-references whose capture is forced (regex_ecma.h DcapForm) are
+    decided in the first pass by byte compares; near-miss forms keep the slow
+    pass.  GPU verdicts and counters against std::regex_match, in front of
+    config 2's rules and alone."""
+    rng = np.random.default_rng(62)
+    for trial in range(8):
+        rules = X.dcap_rules(rng, int(rng.integers(2, 16)))
+        if trial % 2:
+            rules = rules + W.rules(2, n_rules=300)
+        arena, offs = L.pack_http(X.dcap_requests(rng, 20_000))
+        got = _check(rules, arena, offs)
+        assert (got >= 0).any()

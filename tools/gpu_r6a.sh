@@ -10,6 +10,9 @@ step() { local name=$1 secs=$2; shift 2; echo "== $name: $*" >> $OUT/steps.log
   timeout -k 10 $secs "$@" > $OUT/$name.out 2> $OUT/$name.err; local rc=$?; echo "$name rc=$rc" | tee -a $OUT/steps.log; return $rc; }
 step gpu_suite 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit $?
 step bench_default 600 python3 -u bench.py --no-batcher || exit $?
+step bench_ext 400 python3 -u bench.py --extended --no-batcher --no-e2e || exit $?
+step trace_ext 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/trace_ext -o run --output-format csv -- \
+  python3 -u bench.py --extended --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-batcher --no-parity || exit $?
 PASSES=tools/pmc_sq.txt REQS=16000000 BENCH_ARGS="--no-parity" bash tools/gpu_pmc.sh sq_http_$TAG > $OUT/pmc.log 2>&1
 echo "pmc rc=$?" | tee -a $OUT/steps.log
 python3 tools/pmc_summary.py gpurun_out/pmc_sq_http_$TAG > $OUT/sq_summary.txt 2>&1
