@@ -981,7 +981,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
   // value byte; their groups have no automaton, so it must be resident)
   for (uint32_t f = 0; f < nf; ++f) {
     if (!alit[f].on) continue;
-    if (img + alit[f].tab.size() > budget) {
+    if (img + kAlitBloomWords + alit[f].tab.size() > budget) {
       // not resident: the caller compiles again with this field's patterns
       // as plain search groups (a policy that compiled before the alit scan
       // existed still compiles)
@@ -989,7 +989,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       return fail(L7M_ETOOBIG, field_names[f] + ": the literal-anchored pattern table needs " +
                                    std::to_string(4 * alit[f].tab.size()) + " bytes of LDS");
     }
-    fd[f].alit_tab = img_take(alit[f].tab.size());
+    fd[f].alit_tab = img_take(kAlitBloomWords + alit[f].tab.size()) + kAlitBloomWords;  // prefilter bits, then the table
     fd[f].alit_mask = static_cast<uint32_t>(alit[f].tab.size() / 4 - 1);
   }
   // RE2-dialect gram filters (read once per value byte): right after the name table
@@ -1352,6 +1352,12 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     for (size_t e = 1; e < tab.size(); e += 2)
       if (tab[e]) tab[e] = gran[tab[e] - 1] + 1;
     std::memcpy(I + fd[f].alit_tab, tab.data(), tab.size() * 4ull);
+    uint32_t* bloom = I + fd[f].alit_tab - kAlitBloomWords;
+    for (size_t e = 0; e < tab.size(); e += 2)
+      if (tab[e + 1]) {
+        const uint32_t b = alit_bloom_bit(gram_bucket(tab[e]));
+        bloom[b >> 5] |= 1u << (b & 31u);
+      }
     uint32_t* base = (fd[f].alit_lds ? I : P) + fd[f].alit_pats;
     for (size_t i = 0; i < A.pats.size(); ++i) {
       const auto loc = fp_loc[f][A.pats[i]];  // (group, local id)

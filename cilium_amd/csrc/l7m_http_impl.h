@@ -692,25 +692,31 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
       asm volatile("" ::"v"(t));
     }
   };
-  // Windows of 32 positions: the probes of a window only set hit bits (two
-  // per position: the bucket's two entries) -- no candidate work inside the
-  // probe loop, whose iterations differ per lane --; then each hit re-reads
-  // its bucket and runs the compare / residual walk from one call site.
-  // (Processing hits inside the probe loop ran the candidate code once per
-  // word for the whole wave whenever any lane had a hit there.)
+  // Windows of 32 positions.  The probes of a window only set hit bits, one
+  // per position whose gram passes the prefilter (program.h kAlitBloomWords:
+  // one bit of a 2^14-bit map below the bucket table, a dword read and a
+  // bit-field extract) -- no candidate work inside the probe loop, whose
+  // iterations differ per lane --; then each hit reads its bucket, compares
+  // both entries and runs the literal compare / residual walk from one call
+  // site.  (Round 5 read the 16-byte bucket and compared its two entries at
+  // every position: ~22 VALU + a b128 read per position, 39 % of the LDS
+  // cycles bank conflicts; the prefilter is ~10 VALU + a b32 read.)
+  const uint32_t* bloom = c.img + fd.alit_tab - kAlitBloomWords;
+  auto bloom_hit = [&](uint32_t g) -> uint32_t {
+    const uint32_t b = alit_bloom_bit(gram_bucket(g));
+    return __builtin_amdgcn_ubfe(lld(bloom + (b >> 5)), b & 31u, 1);
+  };
   for (uint32_t base = pos & ~3u; base < end; base += 32) {
-    uint64_t hm = 0;
+    uint32_t hm = 0;
     if constexpr (Src::kLds) {
       uint32_t w0 = src.word(base >> 2);
       for (uint32_t i = 0; i < 8 && base + 4 * i < end; ++i) {
         const uint32_t w1 = src.word((base >> 2) + i + 1);
 #pragma unroll
         for (uint32_t sft = 0; sft < 4; ++sft) {
-          const uint32_t q = base + 4 * i + sft, g = __builtin_amdgcn_alignbyte(w1, w0, sft);
-          const bool on = q >= pos && q < end;
-          const u32x4 e = tab[on ? gram_bucket(g) & am : 0u];
-          const uint32_t h = (on && e.y && e.x == g ? 1u : 0u) | (on && e.w && e.z == g ? 2u : 0u);
-          hm |= static_cast<uint64_t>(h) << (2 * (4 * i + sft));
+          const uint32_t q = base + 4 * i + sft;
+          const uint32_t h = bloom_hit(__builtin_amdgcn_alignbyte(w1, w0, sft));
+          hm |= (q >= pos && q < end ? h : 0u) << (4 * i + sft);
         }
         w0 = w1;
       }
@@ -718,18 +724,20 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
       for (uint32_t i = 0; i < 32 && base + i < end; ++i) {
         const uint32_t q = base + i;
         if (q < pos) continue;
-        const uint32_t g = src.word_u(q);
-        const u32x4 e = tab[gram_bucket(g) & am];
-        const uint32_t h = (e.y && e.x == g ? 1u : 0u) | (e.w && e.z == g ? 2u : 0u);
-        hm |= static_cast<uint64_t>(h) << (2 * i);
+        hm |= bloom_hit(src.word_u(q)) << i;
       }
     }
     while (hm) {
-      const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(hm));
+      const uint32_t j = static_cast<uint32_t>(__builtin_ctz(hm));
       hm &= hm - 1;
-      const uint32_t q = base + (j >> 1), g = src.word_u(q);
+      const uint32_t q = base + j, g = src.word_u(q);
       const u32x4 e = tab[gram_bucket(g) & am];
-      candidate(((j & 1u) ? e.w : e.y) - 1, q);
+      uint32_t m2 = (e.y && e.x == g ? 1u : 0u) | (e.w && e.z == g ? 2u : 0u);
+      while (m2) {
+        const uint32_t k = static_cast<uint32_t>(__builtin_ctz(m2));
+        m2 &= m2 - 1;
+        candidate((k ? e.w : e.y) - 1, q);
+      }
     }
   }
 }

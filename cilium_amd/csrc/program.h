@@ -193,6 +193,12 @@ struct AlitRec {
 };
 inline uint32_t alit_rec_granules(uint64_t lit_len) { return 1u + static_cast<uint32_t>((lit_len + 15) / 16); }
 constexpr uint32_t kAlitMinPatterns = 8;          // fewer: plain search groups
+// Prefilter of the alit scan: 2^14 bits right below the bucket table in the
+// LDS image (FieldDesc::alit_tab - kAlitBloomWords); bit alit_bloom_bit(g) is
+// set for every gram g the table holds, so a value position whose gram's bit
+// is clear cannot hit the table and skips its bucket read and compares.
+constexpr uint32_t kAlitBloomWords = 512;
+__host__ __device__ inline uint32_t alit_bloom_bit(uint32_t bucket_hash) { return (bucket_hash >> 8) & 0x3fffu; }
 constexpr uint32_t kAlitMaxLdsBytes = 32u << 10;   // the bucket table
 // Every match of a pattern contains its required literal (regex_re2.cc
 // required_literals), so a value lacking all of a group's chosen 4-byte grams

@@ -122,6 +122,10 @@ class HttpProgram:
             for eg, ep in ((e[0], e[1]), (e[2], e[3])):
                 if not ep or eg != g:
                     continue
+                # the kernel probes the bucket only where the prefilter bit
+                # (program.h kAlitBloomWords) is set: no table gram may lack it
+                bb = (gram_bucket(g) >> 8) & 0x3FFF
+                assert (self.img[tab - 512 + (bb >> 5)] >> (bb & 31)) & 1, "alit prefilter misses a table gram"
                 words, byts = (self.img, self.img_bytes) if fd[13] else (self.w, self.prog_bytes)  # alit_lds
                 r = pats + 4 * (ep - 1)  # AlitRec: header granule, then L's bytes
                 len_k, code, resid, _ = words[r:r + 4]

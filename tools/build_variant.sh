@@ -15,6 +15,10 @@ for f in l7m_kernels l7m_kafka; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-result $FLAGS --offload-arch=gfx950 \
     -munsafe-fp-atomics -c cilium_amd/csrc/$f.hip -o $B/$f.o &
 done
+for F in 0 1 2 3; do  # the HTTP feature-set translation units (Makefile FEAT_OBJS)
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -pthread -Wall -Wno-unused-result $FLAGS --offload-arch=gfx950 \
+    -munsafe-fp-atomics -DL7M_FEAT=$F -c cilium_amd/csrc/l7m_http_feat.hip -o $B/l7m_http_f$F.o &
+done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o variants/$NAME.so $B/*.o -ldl
 echo "built variants/$NAME.so"

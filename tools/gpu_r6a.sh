@@ -11,6 +11,7 @@ step() { local name=$1 secs=$2; shift 2; echo "== $name: $*" >> $OUT/steps.log
 step gpu_suite 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit $?
 step bench_default 600 python3 -u bench.py --no-batcher || exit $?
 step bench_ext 400 python3 -u bench.py --extended --no-batcher --no-e2e || exit $?
+step bench_re2 400 python3 -u bench.py --dialect re2 --no-batcher --no-e2e || exit $?
 step trace_ext 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/trace_ext -o run --output-format csv -- \
   python3 -u bench.py --extended --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-batcher --no-parity || exit $?
 PASSES=tools/pmc_sq.txt REQS=16000000 BENCH_ARGS="--no-parity" bash tools/gpu_pmc.sh sq_http_$TAG > $OUT/pmc.log 2>&1
