@@ -410,6 +410,10 @@ def main():
             "counters_ok": hits_total == expect_hits,
             "host": {"gen_s": gen_s, "h2d_GBps": arena_nbytes / h2d_s / 1e9},
         }
+        tr = res["roofline"]["traffic"]
+        # PMC HBM bytes per launch over the algorithmic bytes: > 1 = re-reads,
+        # < 1 = bytes counted as algorithmic that the kernel never fetched
+        res["roofline"]["traffic_over_algorithmic"] = tr / alg_bytes if tr else None
         log(f"timed {args.steps} steps: {elapsed:.3f} s; kernel {kavg * 1e3:.2f} ms")
         if not args.no_parity and not args.diag:
             log("parity sample (oracle, outside the timed region)")

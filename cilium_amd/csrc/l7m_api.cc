@@ -202,7 +202,9 @@ hipError_t launch_kafka_both(const uint32_t* dprog, const KafkaHeader& h, const 
 }
 
 int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const void* offs, size_t n, void* verdicts,
-           void* hits, hipStream_t stream, uint32_t flags, const void* ids = nullptr) {
+           void* hits, hipStream_t stream, uint32_t flags, const void* ids = nullptr,
+           const DoneSignal* done = nullptr, bool* signalled = nullptr) {
+  if (signalled) *signalled = false;
   auto* rs = const_cast<l7m_ruleset*>(crs);
   const uint32_t* dprog = nullptr;
   int cus = 0;
@@ -227,7 +229,8 @@ int launch(const l7m_ruleset* crs, const void* arena, size_t arena_bytes, const 
       if (dd[k].lit_tab != kNone) flags |= kLaunchLiterals;
     e = launch_http(dprog, h, static_cast<const uint8_t*>(arena), arena_bytes, static_cast<const uint64_t*>(offs),
                     n, static_cast<int32_t*>(verdicts), static_cast<unsigned long long*>(hits),
-                    stream, cus, flags);
+                    stream, cus, flags, done);
+    if (signalled) *signalled = done && n && !h.n_slow && e == hipSuccess;
   } else if (rs->proto == L7M_PROTO_KAFKA) {
     KafkaHeader h;
     std::memcpy(&h, rs->program.data(), sizeof h);
@@ -422,6 +425,19 @@ bool resident_program(l7m_ruleset* rs, const uint32_t** dprog, int* kind, uint32
   KafkaHeader kh;
   std::memcpy(&kh, rs->program.data(), sizeof kh);
   return kafka_resident_ok(kh, kind, stage);
+}
+
+// The batcher's latency path (l7m_batch.cc): l7m_eval_device on device-visible
+// buffers with the kernel's completion signal (l7m_device.h DoneSignal) when
+// one launch decides every request (HTTP without a slow pass); *signalled
+// false means the caller waits on the stream instead.
+int eval_device_signal(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes, const void* d_offs, size_t n,
+                       void* d_verdicts, hipStream_t stream, const DoneSignal& sig, bool* signalled) {
+  *signalled = false;
+  if (!rs || (n && (!d_arena || !d_offs || !d_verdicts))) return L7M_EINVAL;
+  if (reinterpret_cast<uintptr_t>(d_arena) & 15) return L7M_EINVAL;
+  if (rs->proto != L7M_PROTO_HTTP) return launch(rs, d_arena, arena_bytes, d_offs, n, d_verdicts, nullptr, stream, 0);
+  return launch(rs, d_arena, arena_bytes, d_offs, n, d_verdicts, nullptr, stream, 0, nullptr, &sig, signalled);
 }
 
 }  // namespace l7m

@@ -22,7 +22,10 @@
 //     pointers), no staging copies;
 //   * a flusher closes the batch (sets the closed bit, installs a fresh
 //     batch), waits for the reserved slots to be written, enqueues the
-//     kernels on its own stream and polls an event for completion;
+//     kernels on its own stream and polls for completion: HTTP launches
+//     store a sequence number to a pinned host word once every verdict is
+//     visible (round 6, l7m_device.h DoneSignal), other launches are
+//     followed by an event;
 //   * callers spin briefly on the batch's done flag, then sleep on its
 //     condition variable.
 // l7m_batcher_get_profile breaks the per-batch time into these phases.
@@ -46,6 +49,8 @@
 
 namespace l7m {
 bool resident_program(l7m_ruleset* rs, const uint32_t** dprog, int* kind, uint32_t* stage, uint64_t* serial);
+int eval_device_signal(const l7m_ruleset* rs, const void* d_arena, size_t arena_bytes, const void* d_offs, size_t n,
+                       void* d_verdicts, hipStream_t stream, const DoneSignal& sig, bool* signalled);
 void resident_running(int dev, int delta);  // persistent grids leave those CUs out (l7m_api.cc)
 }
 
@@ -380,6 +385,21 @@ struct l7m_batcher {
     hipEvent_t ev = nullptr;
     const bool dev_ok = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
                         hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    // HTTP launches signal their completion by a pinned host word the kernel
+    // stores last (l7m_device.h DoneSignal): polled in place of an event,
+    // whose completion the host sees only after the command processor's
+    // end-of-kernel signal
+    uint32_t* sig_ctr = nullptr;
+    uint32_t* sig_host = nullptr;
+    void* sig_dev = nullptr;
+    uint32_t sig_seq = 0;
+    bool sig_ok = dev_ok && hipMalloc(reinterpret_cast<void**>(&sig_ctr), 64) == hipSuccess &&
+                  hipMemset(sig_ctr, 0, 64) == hipSuccess &&
+                  hipHostMalloc(reinterpret_cast<void**>(&sig_host), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
+                      hipSuccess &&
+                  hipHostGetDevicePointer(&sig_dev, sig_host, 0) == hipSuccess && sig_dev;
+    if (sig_host) std::memset(sig_host, 0, 64);
+    if (std::getenv("L7M_NO_SIGNAL")) sig_ok = false;
     for (;;) {
       Batch* b = cur.load(std::memory_order_acquire);
       const uint64_t s0 = b->resv.load(std::memory_order_acquire);
@@ -463,16 +483,37 @@ struct l7m_batcher {
         if (normal) rc = L7M_OK;
       }
       if (normal) {
-        if (rc == L7M_OK)
+        bool signalled = false;
+        if (rc == L7M_OK && info.proto == L7M_PROTO_HTTP && sig_ok) {
+          const l7m::DoneSignal sg{sig_ctr, static_cast<uint32_t*>(sig_dev), ++sig_seq ? sig_seq : ++sig_seq};
+          rc = l7m::eval_device_signal(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, stream, sg, &signalled);
+        } else if (rc == L7M_OK) {
           rc = info.proto == L7M_PROTO_KAFKA
                    ? l7m_eval_device_ids(r, b->d_arena, bytes, b->d_offs, cnt, b->d_ids, b->d_verd, nullptr, stream, 0)
                    : l7m_eval_device(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, nullptr, stream, 0);
+        }
         t_launch = now_ns();
-        if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
-        if (rc == L7M_OK) {
-          hipError_t q;
-          while ((q = hipEventQuery(ev)) == hipErrorNotReady) cpu_relax();
-          if (q != hipSuccess) rc = L7M_EDEVICE;
+        if (rc == L7M_OK && signalled) {
+          // the kernel's last wave stores sig_seq after every verdict is
+          // visible; the stream is checked now and then so that a failed
+          // launch cannot leave the flusher spinning
+          for (uint32_t spin = 1;; ++spin) {
+            if (__atomic_load_n(sig_host, __ATOMIC_ACQUIRE) == sig_seq) break;
+            if ((spin & 1023) == 0) {
+              const hipError_t q = hipStreamQuery(stream);
+              if (q == hipErrorNotReady) continue;
+              if (q != hipSuccess || __atomic_load_n(sig_host, __ATOMIC_ACQUIRE) != sig_seq) rc = L7M_EDEVICE;
+              break;
+            }
+            cpu_relax();
+          }
+        } else {
+          if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
+          if (rc == L7M_OK) {
+            hipError_t q;
+            while ((q = hipEventQuery(ev)) == hipErrorNotReady) cpu_relax();
+            if (q != hipSuccess) rc = L7M_EDEVICE;
+          }
         }
       }
       const int64_t t_done = now_ns();
@@ -495,6 +536,9 @@ struct l7m_batcher {
         b->cv.notify_all();
       }
     }
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (sig_ctr) (void)hipFree(sig_ctr);
+    if (sig_host) (void)hipHostFree(sig_host);
     if (ev) (void)hipEventDestroy(ev);
     if (stream) (void)hipStreamDestroy(stream);
   }

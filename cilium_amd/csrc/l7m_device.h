@@ -78,9 +78,21 @@ uint32_t http_stage_bytes(const HttpHeader& h);
 // literal tables (DfaDesc::lit_tab), so the kernel instantiation that uses
 // them is launched.
 constexpr uint32_t kLaunchLiterals = 1u << 29;  // L7M_FLAG_DIAG_* use bits 30, 31
+// Completion signal of a first-pass launch (the batcher's latency path):
+// every wave, once its verdicts are visible system-wide, adds one to *ctr
+// (device memory, zero between launches); the last one resets it and stores
+// seq to *flag (pinned host memory, system scope), which the host polls
+// instead of a HIP event.  Only for programs decided in one launch (no slow
+// pass).
+struct DoneSignal {
+  uint32_t* ctr;
+  uint32_t* flag;
+  uint32_t seq;
+};
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                       unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags);
+                       unsigned long long* hits, hipStream_t stream, int num_cus, uint32_t flags,
+                       const DoneSignal* done = nullptr);
 
 // Mailbox of a resident evaluator (l7m_kafka.hip kafka_resident_kernel),
 // in pinned, device-mapped host memory.  The host fills slot seq %

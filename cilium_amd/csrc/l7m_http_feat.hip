@@ -16,10 +16,11 @@ namespace l7m {
 hipError_t L7M_CAT(launch_http_main_f, L7M_FEAT)(int mode, int R, dim3 grid, size_t lds, hipStream_t stream,
                                                  const uint32_t* dprog, const uint8_t* arena, uint64_t arena_bytes,
                                                  const uint64_t* offs, uint64_t n, int32_t* verdicts,
-                                                 unsigned long long* hits, uint32_t stage, uint32_t* slowq) {
+                                                 unsigned long long* hits, uint32_t stage, uint32_t* slowq,
+                                                 DoneSignal done) {
 #define L7M_ONE(M, RR)                                                                                       \
   return launch_one<M, RR, 0, L7M_FEAT>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, \
-                                        stage, nullptr, slowq)
+                                        stage, nullptr, slowq, done)
 #define L7M_MODES(RR)                             \
   {                                               \
     if (mode == kNoHits) L7M_ONE(kNoHits, RR);    \

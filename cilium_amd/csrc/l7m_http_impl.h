@@ -1392,7 +1392,8 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
                                                int32_t* __restrict__ verdicts, unsigned long long* __restrict__ hits,
                                                uint32_t stage, uint32_t* __restrict__ scratch,
                                                uint32_t* __restrict__ slowq, bool load_image, uint32_t part,
-                                               uint32_t nparts, uint32_t wave_index, uint32_t wave_count) {
+                                               uint32_t nparts, uint32_t wave_index, uint32_t wave_count,
+                                               DoneSignal done = DoneSignal{nullptr, nullptr, 0}) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -1401,6 +1402,23 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
   uint32_t* ctr = smem + h.lds_image_words;  // LDS hit counters (kLdsHits)
   uint32_t* col = ctr + (kHits == kLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);  // LDS code columns (!kReg)
   uint8_t* stg = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock)) + wv * (stage + 16u);
+  // This wave's contiguous share of the batch, consumed in tiles of <= 64
+  // records (wave wave_index of wave_count).  The first tile's offsets are
+  // requested before the LDS image is loaded, so the two latencies overlap
+  // (small batches: the offsets may sit in pinned host memory, across PCIe).
+  const uint64_t gw = wave_index;
+  const uint64_t nw = wave_count;
+  const uint64_t end = n * (gw + 1) / nw;
+  auto load_offs = [&](uint64_t cur, uint64_t* o, uint64_t* onext) {
+    *o = 0;
+    *onext = 0;
+    if (cur < end && lane < end - cur) {
+      *o = offs[cur + lane];
+      *onext = cur + lane + 1 < n ? offs[cur + lane + 1] : arena_bytes;
+    }
+  };
+  uint64_t o1, n1, o2, n2;
+  load_offs(n * gw / nw, &o1, &n1);
   if (load_image) {
     const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
     uint4* l = reinterpret_cast<uint4*>(img);
@@ -1436,24 +1454,11 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
     }
   };
 
-  // This wave's contiguous share of the batch, consumed in tiles of <= 64
-  // records.  Software pipeline per wave: while tile t is evaluated from the
-  // LDS stage, tile t+1's bytes and tile t+2's offsets are already in flight.
-  // this wave's share of the batch: wave wave_index of wave_count
-  const uint64_t gw = wave_index;
-  const uint64_t nw = wave_count;
-  const uint64_t end = n * (gw + 1) / nw;
+  // Software pipeline per wave: while tile t is evaluated from the LDS
+  // stage, tile t+1's bytes and tile t+2's offsets are already in flight.
   struct Tile {
     uint64_t cur, o, onext, base;
     uint32_t k, bytes, take;
-  };
-  auto load_offs = [&](uint64_t cur, uint64_t* o, uint64_t* onext) {
-    *o = 0;
-    *onext = 0;
-    if (cur < end && lane < end - cur) {
-      *o = offs[cur + lane];
-      *onext = cur + lane + 1 < n ? offs[cur + lane + 1] : arena_bytes;
-    }
   };
   auto plan = [&](uint64_t cur, uint64_t o, uint64_t onext) -> Tile {
     Tile t;
@@ -1513,8 +1518,6 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
           __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(arena + o + 128ull * j), junk, 4, 0, 0);
     }
   };
-  uint64_t o1, n1, o2, n2;
-  load_offs(n * gw / nw, &o1, &n1);
   Tile t = plan(n * gw / nw, o1, n1);
   issue_bytes(t);
   load_offs(t.cur + t.take, &o2, &n2);
@@ -1613,6 +1616,14 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
     for (uint32_t i = tid; i < n_ctr; i += kBlock)
       if (ctr[i]) atomicAdd(hits + i, static_cast<unsigned long long>(ctr[i]));
   }
+  if (done.flag) {  // (l7m_device.h DoneSignal)
+    __threadfence_system();  // this wave's verdict stores (and counters) are visible system-wide
+    if (lane == 0 && atomicAdd(done.ctr, 1u) == wave_count - 1u) {
+      __threadfence_system();
+      __hip_atomic_store(done.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done.flag, done.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 template <int kHits, int kReg, int kAblate, int kFeat>
@@ -1621,10 +1632,11 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
                                                            const uint64_t* __restrict__ offs, uint64_t n,
                                                            int32_t* __restrict__ verdicts,
                                                            unsigned long long* __restrict__ hits, uint32_t stage,
-                                                           uint32_t* __restrict__ scratch, uint32_t* __restrict__ slowq) {
+                                                           uint32_t* __restrict__ scratch, uint32_t* __restrict__ slowq,
+                                                           DoneSignal done) {
   http_eval_body<kHits, kReg, kAblate, kFeat>(prog, arena, arena_bytes, offs, n, verdicts, hits, stage, scratch, slowq,
                                              true, blockIdx.x, gridDim.x, blockIdx.x * kWaves + (threadIdx.x >> 6),
-                                             gridDim.x * kWaves);
+                                             gridDim.x * kWaves, done);
 }
 
 // Second pass over the requests the first pass deferred (a slow-path rule may
@@ -1736,14 +1748,14 @@ template <int kHits, int kReg, int kAblate = 0, int kFeat = 0>
 hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, uint32_t stage, uint32_t* scratch = nullptr,
-                       uint32_t* slowq = nullptr) {
+                       uint32_t* slowq = nullptr, DoneSignal done = DoneSignal{nullptr, nullptr, 0}) {
   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU); set per device
   // and instantiation, thread-safely (l7m_device.h)
   const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate, kFeat>),
                                          kHttpLdsBytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate, kFeat>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
-                     offs, n, verdicts, hits, stage, scratch, slowq);
+                     offs, n, verdicts, hits, stage, scratch, slowq, done);
   return hipGetLastError();
 }
 

@@ -30,7 +30,8 @@ namespace l7m {
 #define L7M_FEAT_DECL(F)                                                                                            \
   hipError_t launch_http_main_f##F(int mode, int R, dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog,  \
                                    const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs, uint64_t n,        \
-                                   int32_t* verdicts, unsigned long long* hits, uint32_t stage, uint32_t* slowq);      \
+                                   int32_t* verdicts, unsigned long long* hits, uint32_t stage, uint32_t* slowq,       \
+                                   DoneSignal done);                                                                   \
   hipError_t launch_http_slow_f##F(int R, int tier, const HttpHeader& h, uint32_t blocks, hipStream_t stream,         \
                                    const uint32_t* dprog, const uint8_t* arena, uint64_t arena_bytes,                  \
                                    const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,      \
@@ -63,7 +64,7 @@ hipError_t launch_resident(ResidentBox* dbox, uint64_t first_seq, int kind, uint
 
 hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t* arena, uint64_t arena_bytes,
                        const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,
-                       hipStream_t stream, int num_cus, uint32_t flags) {
+                       hipStream_t stream, int num_cus, uint32_t flags, const DoneSignal* done) {
   if (n == 0) return hipSuccess;
   const uint32_t stage = http_stage_bytes(h);
   if (stage == 0) return hipErrorInvalidValue;
@@ -91,12 +92,13 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
     const size_t bytes = static_cast<size_t>(h.n_dfas ? h.n_dfas : 1) * grid.x * kBlock * 4u;
     hipError_t e = scratch_alloc_async(reinterpret_cast<void**>(&scratch), bytes, stream);
     if (e != hipSuccess) return e;
+    const DoneSignal sig = done ? *done : DoneSignal{nullptr, nullptr, 0};
     if (mode == kNoHits) e = launch_one<kNoHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts,
-                                                     hits, stage, scratch);
+                                                     hits, stage, scratch, nullptr, sig);
     else if (mode == kLdsHits) e = launch_one<kLdsHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n,
-                                                            verdicts, hits, stage, scratch);
+                                                            verdicts, hits, stage, scratch, nullptr, sig);
     else e = launch_one<kGlobalHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage,
-                                         scratch);
+                                         scratch, nullptr, sig);
     const hipError_t e2 = hipFreeAsync(scratch, stream);
     return e != hipSuccess ? e : e2;
   }
@@ -142,7 +144,10 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
                                                            launch_http_main_f2, launch_http_main_f3};
   static decltype(&launch_http_slow_f0) const slows[4] = {launch_http_slow_f0, launch_http_slow_f1,
                                                            launch_http_slow_f2, launch_http_slow_f3};
-  hipError_t e = mains[feat](mode, R, grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage, slowq);
+  // the completion signal only where this launch decides every request
+  const DoneSignal sig = done && !h.n_slow ? *done : DoneSignal{nullptr, nullptr, 0};
+  hipError_t e =
+      mains[feat](mode, R, grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage, slowq, sig);
   if (h.n_slow) {
     for (int tier = 1; tier <= 2 && e == hipSuccess; ++tier)
       e = slows[feat](R, tier, h, tier == 1 ? blocks1 : blocks2, stream, dprog, arena, arena_bytes, offs, n, verdicts,

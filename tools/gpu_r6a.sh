@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 step() { local name=$1 secs=$2; shift 2; echo "== $name: $*" >> $OUT/steps.log
   timeout -k 10 $secs "$@" > $OUT/$name.out 2> $OUT/$name.err; local rc=$?; echo "$name rc=$rc" | tee -a $OUT/steps.log; return $rc; }
 step gpu_suite 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit $?
-step bench_default 600 python3 -u bench.py --no-batcher || exit $?
+step bench_default 600 python3 -u bench.py || exit $?
 step bench_ext 400 python3 -u bench.py --extended --no-batcher --no-e2e || exit $?
 step bench_re2 400 python3 -u bench.py --dialect re2 --no-batcher --no-e2e || exit $?
 step trace_ext 400 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/trace_ext -o run --output-format csv -- \
