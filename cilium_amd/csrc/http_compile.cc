@@ -929,7 +929,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
     for (const auto& g : groups[f]) any_search |= g.search;
   // (search programs keep their end codes in a global scratch, l7m_kernels.hip)
   const uint64_t codes_bytes = ndfa > kHttpRegDfas && !any_search ? 4ull * kHttpBlock * ndfa : 0;
-  const uint64_t ctr_bytes = n + 2 <= kMaxLdsCounters ? 4ull * ((n + 2 + 3) & ~uint64_t(3)) : 0;
+  const uint64_t ctr_bytes = !kSliceHits && n + 2 <= kMaxLdsCounters ? 4ull * ((n + 2 + 3) & ~uint64_t(3)) : 0;
   const uint64_t stage_bytes = static_cast<uint64_t>(kHttpWaves) * (kHttpMinStage + 16);
   uint64_t img = 0;  // image words
   auto img_take = [&](uint64_t words) {

@@ -17,10 +17,10 @@ hipError_t L7M_CAT(launch_http_main_f, L7M_FEAT)(int mode, int R, dim3 grid, siz
                                                  const uint32_t* dprog, const uint8_t* arena, uint64_t arena_bytes,
                                                  const uint64_t* offs, uint64_t n, int32_t* verdicts,
                                                  unsigned long long* hits, uint32_t stage, uint32_t* slowq,
-                                                 DoneSignal done) {
+                                                 DoneSignal done, uint32_t* hslice) {
 #define L7M_ONE(M, RR)                                                                                       \
   return launch_one<M, RR, 0, L7M_FEAT>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, \
-                                        stage, nullptr, slowq, done)
+                                        stage, nullptr, slowq, done, hslice)
 #define L7M_MODES(RR)                             \
   {                                               \
     if (mode == kNoHits) L7M_ONE(kNoHits, RR);    \

@@ -19,7 +19,7 @@ namespace {
 constexpr uint32_t kWaves = kHttpWaves;
 constexpr uint32_t kBlock = kHttpBlock;
 constexpr uint32_t kMaxStage = kHttpMaxStage;  // bytes of records staged per wave and tile
-constexpr uint32_t kCopyIters = kMaxStage / 1024;
+constexpr uint32_t kCopyIters = (kMaxStage + 1023) / 1024;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifdef L7M_PROF
 constexpr bool kProf = true;  // diagnostic build: wave timeline printed by two waves
@@ -1393,14 +1393,17 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
                                                uint32_t stage, uint32_t* __restrict__ scratch,
                                                uint32_t* __restrict__ slowq, bool load_image, uint32_t part,
                                                uint32_t nparts, uint32_t wave_index, uint32_t wave_count,
-                                               DoneSignal done = DoneSignal{nullptr, nullptr, 0}) {
+                                               DoneSignal done = DoneSignal{nullptr, nullptr, 0},
+                                               uint32_t* __restrict__ hslice = nullptr) {
   extern __shared__ __align__(16) uint32_t smem[];
   const HttpHeader& h = *reinterpret_cast<const HttpHeader*>(prog);
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   uint32_t* img = smem;
   const uint32_t n_ctr = h.n_rules + 2;
-  uint32_t* ctr = smem + h.lds_image_words;  // LDS hit counters (kLdsHits)
-  uint32_t* col = ctr + (kHits == kLdsHits ? ((n_ctr + 3u) & ~3u) : 0u);  // LDS code columns (!kReg)
+  // hit counters (kLdsHits): LDS, or (kSliceHits) this workgroup's global slice
+  uint32_t* ctr = kSliceHits ? hslice + static_cast<uint64_t>(part) * ((n_ctr + 63u) & ~63u) : smem + h.lds_image_words;
+  uint32_t* col = (kSliceHits ? smem + h.lds_image_words : ctr) +
+                  (kHits == kLdsHits && !kSliceHits ? ((n_ctr + 3u) & ~3u) : 0u);  // LDS code columns (!kReg)
   uint8_t* stg = reinterpret_cast<uint8_t*>(col + (kReg ? 0u : h.n_dfas * kBlock)) + wv * (stage + 16u);
   // This wave's contiguous share of the batch, consumed in tiles of <= 64
   // records (wave wave_index of wave_count).  The first tile's offsets are
@@ -1425,7 +1428,10 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
     for (uint32_t i = tid; i < h.lds_image_words / 4u; i += kBlock) l[i] = g[i];
   }
   if (kHits == kLdsHits)
-    for (uint32_t i = tid; i < n_ctr; i += kBlock) ctr[i] = 0;
+    for (uint32_t i = tid; i < n_ctr; i += kBlock) {
+      if constexpr (kSliceHits) __hip_atomic_store(ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else ctr[i] = 0;
+    }
   __syncthreads();
 
   Ctx c;
@@ -1579,9 +1585,13 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
       if (kHits == kLdsHits) {
         // denies / errors are common: one add per wave for them
         const uint64_t dm = __ballot(slot == 0u), em = __ballot(slot == 1u);
-        if (lane == 0 && dm) atomicAdd(ctr, static_cast<uint32_t>(__popcll(dm)));
-        if (lane == 0 && em) atomicAdd(ctr + 1, static_cast<uint32_t>(__popcll(em)));
-        if (slot != kNone && slot >= 2u) atomicAdd(ctr + slot, 1u);
+        auto add = [&](uint32_t i, uint32_t x) {
+          if constexpr (kSliceHits) (void)__hip_atomic_fetch_add(ctr + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          else atomicAdd(ctr + i, x);
+        };
+        if (lane == 0 && dm) add(0, static_cast<uint32_t>(__popcll(dm)));
+        if (lane == 0 && em) add(1, static_cast<uint32_t>(__popcll(em)));
+        if (slot != kNone && slot >= 2u) add(slot, 1u);
       } else {
         count_slot(hits, slot, slot != kNone);
       }
@@ -1613,8 +1623,10 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
   }
   if (kHits == kLdsHits) {
     __syncthreads();
-    for (uint32_t i = tid; i < n_ctr; i += kBlock)
-      if (ctr[i]) atomicAdd(hits + i, static_cast<unsigned long long>(ctr[i]));
+    for (uint32_t i = tid; i < n_ctr; i += kBlock) {
+      const uint32_t x = kSliceHits ? __hip_atomic_load(ctr + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ctr[i];
+      if (x) atomicAdd(hits + i, static_cast<unsigned long long>(x));
+    }
   }
   if (done.flag) {  // (l7m_device.h DoneSignal)
     __threadfence_system();  // this wave's verdict stores (and counters) are visible system-wide
@@ -1633,10 +1645,10 @@ __global__ __launch_bounds__(kBlock) L7M_HTTP_OCC void http_eval_kernel(const ui
                                                            int32_t* __restrict__ verdicts,
                                                            unsigned long long* __restrict__ hits, uint32_t stage,
                                                            uint32_t* __restrict__ scratch, uint32_t* __restrict__ slowq,
-                                                           DoneSignal done) {
+                                                           DoneSignal done, uint32_t* __restrict__ hslice) {
   http_eval_body<kHits, kReg, kAblate, kFeat>(prog, arena, arena_bytes, offs, n, verdicts, hits, stage, scratch, slowq,
                                              true, blockIdx.x, gridDim.x, blockIdx.x * kWaves + (threadIdx.x >> 6),
-                                             gridDim.x * kWaves, done);
+                                             gridDim.x * kWaves, done, hslice);
 }
 
 // Second pass over the requests the first pass deferred (a slow-path rule may
@@ -1748,14 +1760,15 @@ template <int kHits, int kReg, int kAblate = 0, int kFeat = 0>
 hipError_t launch_one(dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog, const uint8_t* arena,
                        uint64_t arena_bytes, const uint64_t* offs, uint64_t n, int32_t* verdicts,
                        unsigned long long* hits, uint32_t stage, uint32_t* scratch = nullptr,
-                       uint32_t* slowq = nullptr, DoneSignal done = DoneSignal{nullptr, nullptr, 0}) {
+                       uint32_t* slowq = nullptr, DoneSignal done = DoneSignal{nullptr, nullptr, 0},
+                       uint32_t* hslice = nullptr) {
   // allow > 64 KiB of dynamic LDS (gfx950: 160 KiB per CU); set per device
   // and instantiation, thread-safely (l7m_device.h)
   const hipError_t e = set_lds_attr_once(reinterpret_cast<const void*>(http_eval_kernel<kHits, kReg, kAblate, kFeat>),
                                          kHttpLdsBytes);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((http_eval_kernel<kHits, kReg, kAblate, kFeat>), grid, dim3(kBlock), lds, stream, dprog, arena, arena_bytes,
-                     offs, n, verdicts, hits, stage, scratch, slowq, done);
+                     offs, n, verdicts, hits, stage, scratch, slowq, done, hslice);
   return hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ namespace l7m {
   hipError_t launch_http_main_f##F(int mode, int R, dim3 grid, size_t lds, hipStream_t stream, const uint32_t* dprog,  \
                                    const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs, uint64_t n,        \
                                    int32_t* verdicts, unsigned long long* hits, uint32_t stage, uint32_t* slowq,       \
-                                   DoneSignal done);                                                                   \
+                                   DoneSignal done, uint32_t* hslice);                                                 \
   hipError_t launch_http_slow_f##F(int R, int tier, const HttpHeader& h, uint32_t blocks, hipStream_t stream,         \
                                    const uint32_t* dprog, const uint8_t* arena, uint64_t arena_bytes,                  \
                                    const uint64_t* offs, uint64_t n, int32_t* verdicts, unsigned long long* hits,      \
@@ -44,7 +44,7 @@ L7M_FEAT_DECL(3)
 
 size_t http_lds_bytes(const HttpHeader& h, uint32_t stage) {
   const bool reg = h.n_dfas <= kRegDfas || h.search;  // search programs: codes in global scratch
-  const size_t ctr = h.n_rules + 2 <= kMaxLdsCounters ? ((h.n_rules + 2 + 3) & ~size_t(3)) : 0;
+  const size_t ctr = !kSliceHits && h.n_rules + 2 <= kMaxLdsCounters ? ((h.n_rules + 2 + 3) & ~size_t(3)) : 0;
   return 4u * (static_cast<size_t>(h.lds_image_words) + ctr + (reg ? 0u : static_cast<size_t>(h.n_dfas) * kBlock)) +
          static_cast<size_t>(kWaves) * (stage + 16u);
 }
@@ -84,6 +84,17 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
     return launch_one<kNoHits, 8, 1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage);
   }
   const int mode = !hits ? kNoHits : (h.n_rules + 2 <= kMaxLdsCounters ? kLdsHits : kGlobalHits);
+  // (kSliceHits) the workgroups' global counter slices, stream-ordered
+  uint32_t* hslice = nullptr;
+  if (kSliceHits && mode == kLdsHits) {
+    const size_t bytes = static_cast<size_t>(grid.x) * ((h.n_rules + 2 + 63) & ~63u) * 4u;
+    const hipError_t e = scratch_alloc_async(reinterpret_cast<void**>(&hslice), bytes, stream);
+    if (e != hipSuccess) return e;
+  }
+  auto free_slice = [&](hipError_t e) {
+    const hipError_t e2 = hslice ? hipFreeAsync(hslice, stream) : hipSuccess;
+    return e != hipSuccess ? e : e2;
+  };
   if (h.search) {
     // RE2-dialect programs (search automata, program.h kDfaSearch): their own
     // instantiation, end codes in a stream-ordered global scratch column per
@@ -91,16 +102,16 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
     uint32_t* scratch = nullptr;
     const size_t bytes = static_cast<size_t>(h.n_dfas ? h.n_dfas : 1) * grid.x * kBlock * 4u;
     hipError_t e = scratch_alloc_async(reinterpret_cast<void**>(&scratch), bytes, stream);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) return free_slice(e);
     const DoneSignal sig = done ? *done : DoneSignal{nullptr, nullptr, 0};
     if (mode == kNoHits) e = launch_one<kNoHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts,
-                                                     hits, stage, scratch, nullptr, sig);
+                                                     hits, stage, scratch, nullptr, sig, hslice);
     else if (mode == kLdsHits) e = launch_one<kLdsHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n,
-                                                            verdicts, hits, stage, scratch, nullptr, sig);
+                                                            verdicts, hits, stage, scratch, nullptr, sig, hslice);
     else e = launch_one<kGlobalHits, -1>(grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage,
-                                         scratch, nullptr, sig);
+                                         scratch, nullptr, sig, hslice);
     const hipError_t e2 = hipFreeAsync(scratch, stream);
-    return e != hipSuccess ? e : e2;
+    return free_slice(e != hipSuccess ? e : e2);
   }
   // end codes in 4 or 8 registers, or in LDS columns
   const bool lit = (flags & kLaunchLiterals) != 0;
@@ -129,7 +140,7 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
     if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(buf) + 512 + qbytes, 0, 4, stream);
     if (e != hipSuccess) {
       if (buf) (void)hipFreeAsync(buf, stream);
-      return e;
+      return free_slice(e);
     }
     work = static_cast<uint32_t*>(buf);
     slowq = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(buf) + 512);
@@ -146,8 +157,8 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
                                                            launch_http_slow_f2, launch_http_slow_f3};
   // the completion signal only where this launch decides every request
   const DoneSignal sig = done && !h.n_slow ? *done : DoneSignal{nullptr, nullptr, 0};
-  hipError_t e =
-      mains[feat](mode, R, grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage, slowq, sig);
+  hipError_t e = mains[feat](mode, R, grid, lds, stream, dprog, arena, arena_bytes, offs, n, verdicts, hits, stage,
+                             slowq, sig, hslice);
   if (h.n_slow) {
     for (int tier = 1; tier <= 2 && e == hipSuccess; ++tier)
       e = slows[feat](R, tier, h, tier == 1 ? blocks1 : blocks2, stream, dprog, arena, arena_bytes, offs, n, verdicts,
@@ -155,7 +166,7 @@ hipError_t launch_http(const uint32_t* dprog, const HttpHeader& h, const uint8_t
     const hipError_t e2 = hipFreeAsync(buf, stream);
     if (e == hipSuccess) e = e2;
   }
-  return e;
+  return free_slice(e);
 }
 
 }  // namespace l7m

@@ -151,8 +151,18 @@ constexpr uint32_t kHttpWgPerCu = L7M_HTTP_WG_PER_CU;
 constexpr uint32_t kHttpLdsBytes = kLdsBytes / kHttpWgPerCu;  // LDS of one HTTP workgroup
 constexpr uint32_t kHttpRegDfas = 8;             // <= 8 value DFAs: end codes in registers
 constexpr uint32_t kMaxLdsCounters = 8192;       // per-rule hit counters kept in LDS up to this
+#ifndef L7M_SLICE_HITS
+#define L7M_SLICE_HITS 0
+#endif
+// (experiment) the per-workgroup hit counters in a global slice per
+// workgroup (workgroup-scope atomics in L2) instead of LDS, so the record
+// stage gets their LDS
+constexpr bool kSliceHits = L7M_SLICE_HITS != 0;
 constexpr uint32_t kHttpMinStage = 2048;         // smallest record stage per wave (bytes)
-constexpr uint32_t kHttpMaxStage = 8192;         // largest record stage per wave (bytes)
+#ifndef L7M_HTTP_MAX_STAGE
+#define L7M_HTTP_MAX_STAGE 8192
+#endif
+constexpr uint32_t kHttpMaxStage = L7M_HTTP_MAX_STAGE;  // largest record stage per wave (bytes)
 constexpr uint32_t kMaxLdsCtmaskWords = 256;     // candidate-presence bitmask kept in LDS up to this
 
 struct FieldDesc {
