@@ -117,30 +117,34 @@ def test_forced_capture_backreferences(gpu):
 
 def test_step_budget_outcomes_pinned_against_the_oracle(gpu):
     """The executor's step budgets (regex_vm.h: tier 1 2^22, tier 2 2^25
-    steps) on exponential backtracking, /(a|a)*\\1b over /a^n c.  std::regex
-    (no step limit) explores all 2^n paths and decides every n (rule 1 then
-    allows); the GPU equals it wherever the host build of the executor decides
-    within the tier-2 budget, and answers -3 (L7M_VERDICT_UNSUPPORTED) exactly
-    where that budget runs out -- never a wrong allow or deny."""
+    steps) on exponential backtracking the first pass cannot rule out:
+    /((a|a)*)c\\1d over /a^n c a^(n+1) d.  The superset automaton accepts
+    (the reference group becomes a^*), and std::regex (no step limit) tries
+    all 2^n ways to match a^n before it fails, so rule 1 allows every n.
+    The GPU equals it wherever the host build of the executor decides within
+    the tier-2 budget, and answers -3 (L7M_VERDICT_UNSUPPORTED) exactly where
+    that budget runs out -- never a wrong allow or deny."""
     import time
     from program_interp import _VM, VM_SCRATCH_WORDS, VM_MAX_STEPS, VM_LIMIT
-    pat = "/(a|a)*\\1b"
+    pat = "/((a|a)*)c\\1d"
     rules = [L.PortRuleHTTP(Path=pat), L.PortRuleHTTP(Path="/.*")]
     sizes = list(range(12, 25, 2))
-    reqs = [L.HTTPRequest("GET", "/" + "a" * n + "c") for n in sizes]
+    subj = ["/" + "a" * n + "c" + "a" * (n + 1) + "d" for n in sizes]
+    reqs = [L.HTTPRequest("GET", x) for x in subj]
     arena, offs = L.pack_http(reqs)
     rs = L.RuleSet.compile_http(rules)
     got = rs.eval(arena, offs)
     t0 = time.perf_counter()
     exp = HttpOracle(rules, prefilter=False).eval(arena, offs)
-    assert time.perf_counter() - t0 < 60
+    assert time.perf_counter() - t0 < 120
     P = HttpProgram(rs.program())
     h = P.h
+    assert h["n_slow"] == 1 and not P.dcaps  # a loop inside the group: not a forced capture
     so, _ = P.w[h["off_slow"]: h["off_slow"] + 2]
     prog = P.prog[P.w[h["off_pool"] + so + 1]:]
     limited = []
     for i, n in enumerate(sizes):
-        s = ("/" + "a" * n + "c").encode()
+        s = subj[i].encode()
         r = _VM.vm_host_match(prog.ctypes.data, s, len(s), VM_SCRATCH_WORDS, VM_MAX_STEPS)
         assert exp[i] == 1  # the reference decides: rule 0 fails, rule 1 allows
         if r == VM_LIMIT:
