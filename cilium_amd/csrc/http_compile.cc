@@ -1353,7 +1353,7 @@ CompileResult compile_http_core(const l7m_http_rule* rules, size_t n, const Poli
       if (tab[e]) tab[e] = gran[tab[e] - 1] + 1;
     std::memcpy(I + fd[f].alit_tab, tab.data(), tab.size() * 4ull);
     uint32_t* bloom = I + fd[f].alit_tab - kAlitBloomWords;
-    for (size_t e = 0; e < tab.size(); e += 2)
+    for (size_t e = 0; kAlitBloomWords && e < tab.size(); e += 2)
       if (tab[e + 1]) {
         const uint32_t b = alit_bloom_bit(gram_bucket(tab[e]));
         bloom[b >> 5] |= 1u << (b & 31u);

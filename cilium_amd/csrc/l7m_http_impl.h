@@ -706,6 +706,12 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
     const uint32_t b = alit_bloom_bit(gram_bucket(g));
     return __builtin_amdgcn_ubfe(lld(bloom + (b >> 5)), b & 31u, 1);
   };
+  // without the prefilter (kAlitBloomBits 0, round 5): the bucket itself
+  auto bucket_hit = [&](uint32_t g) -> uint32_t {
+    const u32x4 e = tab[gram_bucket(g) & am];
+    return (e.y && e.x == g) || (e.w && e.z == g) ? 1u : 0u;
+  };
+  auto probe = [&](uint32_t g) -> uint32_t { return kAlitBloomBits ? bloom_hit(g) : bucket_hit(g); };
   for (uint32_t base = pos & ~3u; base < end; base += 32) {
     uint32_t hm = 0;
     if constexpr (Src::kLds) {
@@ -715,7 +721,7 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
 #pragma unroll
         for (uint32_t sft = 0; sft < 4; ++sft) {
           const uint32_t q = base + 4 * i + sft;
-          const uint32_t h = bloom_hit(__builtin_amdgcn_alignbyte(w1, w0, sft));
+          const uint32_t h = probe(__builtin_amdgcn_alignbyte(w1, w0, sft));
           hm |= (q >= pos && q < end ? h : 0u) << (4 * i + sft);
         }
         w0 = w1;
@@ -724,7 +730,7 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
       for (uint32_t i = 0; i < 32 && base + i < end; ++i) {
         const uint32_t q = base + i;
         if (q < pos) continue;
-        hm |= bloom_hit(src.word_u(q)) << i;
+        hm |= probe(src.word_u(q)) << i;
       }
     }
     while (hm) {

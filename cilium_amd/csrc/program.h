@@ -207,8 +207,14 @@ constexpr uint32_t kAlitMinPatterns = 8;          // fewer: plain search groups
 // LDS image (FieldDesc::alit_tab - kAlitBloomWords); bit alit_bloom_bit(g) is
 // set for every gram g the table holds, so a value position whose gram's bit
 // is clear cannot hit the table and skips its bucket read and compares.
-constexpr uint32_t kAlitBloomWords = 512;
-__host__ __device__ inline uint32_t alit_bloom_bit(uint32_t bucket_hash) { return (bucket_hash >> 8) & 0x3fffu; }
+#ifndef L7M_ALIT_BLOOM_BITS
+#define L7M_ALIT_BLOOM_BITS 14  // log2 of the prefilter's bits; 0: no prefilter (every position reads its bucket)
+#endif
+constexpr uint32_t kAlitBloomBits = L7M_ALIT_BLOOM_BITS;
+constexpr uint32_t kAlitBloomWords = kAlitBloomBits ? (1u << kAlitBloomBits) / 32u : 0u;
+__host__ __device__ inline uint32_t alit_bloom_bit(uint32_t bucket_hash) {
+  return (bucket_hash >> 8) & ((1u << kAlitBloomBits) - 1u);
+}
 constexpr uint32_t kAlitMaxLdsBytes = 32u << 10;   // the bucket table
 // Every match of a pattern contains its required literal (regex_re2.cc
 // required_literals), so a value lacking all of a group's chosen 4-byte grams
