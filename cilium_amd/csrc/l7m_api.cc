@@ -69,6 +69,12 @@ int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
     cached_cus = prop.multiProcessorCount;
   }
   *cus = cached_cus;
+  // fast path without the lock once the program is on this device (the
+  // batcher's flushers launch concurrently on one rule set)
+  if (void* q = __atomic_load_n(&rs->dprog[dev], __ATOMIC_ACQUIRE)) {
+    *out = static_cast<const uint32_t*>(q);
+    return L7M_OK;
+  }
   std::lock_guard<std::mutex> g(rs->mu);
   if (!rs->dprog[dev]) {
     void* p = nullptr;
@@ -78,7 +84,7 @@ int device_program(l7m_ruleset* rs, const uint32_t** out, int* cus) {
       (void)hipFree(p);
       return L7M_EDEVICE;
     }
-    rs->dprog[dev] = p;
+    __atomic_store_n(&rs->dprog[dev], p, __ATOMIC_RELEASE);
   }
   *out = static_cast<const uint32_t*>(rs->dprog[dev]);
   return L7M_OK;

@@ -22,13 +22,22 @@ inline hipError_t set_lds_attr_once(const void* fn, uint32_t bytes) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
+  // per-thread cache of the (kernel, device) pairs already done: the
+  // batcher's flushers launch per batch and would contend on the mutex
+  static thread_local const void* last_fn = nullptr;
+  static thread_local int last_dev = -1;
+  if (fn == last_fn && dev == last_dev) return hipSuccess;
   static std::mutex mu;
   static std::set<std::pair<const void*, int>> done;
   std::lock_guard<std::mutex> g(mu);
-  if (done.count({fn, dev})) return hipSuccess;
-  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
-  if (e == hipSuccess) done.insert({fn, dev});
-  return e;
+  if (!done.count({fn, dev})) {
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+    if (e != hipSuccess) return e;
+    done.insert({fn, dev});
+  }
+  last_fn = fn;
+  last_dev = dev;
+  return hipSuccess;
 }
 
 // Stream-ordered scratch (the slow pass's executor stacks, the search
