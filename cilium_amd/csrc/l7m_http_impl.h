@@ -693,14 +693,16 @@ __device__ __forceinline__ void alit_scan(const Ctx& c, const FieldDesc& fd, con
     }
   };
   // Windows of 32 positions.  The probes of a window only set hit bits, one
-  // per position whose gram passes the prefilter (program.h kAlitBloomWords:
-  // one bit of a 2^14-bit map below the bucket table, a dword read and a
-  // bit-field extract) -- no candidate work inside the probe loop, whose
-  // iterations differ per lane --; then each hit reads its bucket, compares
-  // both entries and runs the literal compare / residual walk from one call
-  // site.  (Round 5 read the 16-byte bucket and compared its two entries at
-  // every position: ~22 VALU + a b128 read per position, 39 % of the LDS
-  // cycles bank conflicts; the prefilter is ~10 VALU + a b32 read.)
+  // per position whose gram hits its bucket -- no candidate work inside the
+  // probe loop, whose iterations differ per lane --; then each hit re-reads
+  // its bucket and runs the literal compare / residual walk of each matching
+  // entry from one call site.  The optional prefilter (program.h
+  // L7M_ALIT_BLOOM_BITS: one bit of a 2^bits map below the bucket table per
+  // position, a dword read and a bit-field extract instead of the 16-byte
+  // bucket read and two compares) measured slower on config 2 (round 6,
+  // profiles/r06/ab_re2_prefilter_*: 2^14 bits 13.4 ms, 2^12 14.3 ms, off
+  // 12.9 ms): its LDS costs record stage, and its false positives re-read
+  // buckets, so it is off by default.
   const uint32_t* bloom = c.img + fd.alit_tab - kAlitBloomWords;
   auto bloom_hit = [&](uint32_t g) -> uint32_t {
     const uint32_t b = alit_bloom_bit(gram_bucket(g));

@@ -208,7 +208,7 @@ constexpr uint32_t kAlitMinPatterns = 8;          // fewer: plain search groups
 // set for every gram g the table holds, so a value position whose gram's bit
 // is clear cannot hit the table and skips its bucket read and compares.
 #ifndef L7M_ALIT_BLOOM_BITS
-#define L7M_ALIT_BLOOM_BITS 14  // log2 of the prefilter's bits; 0: no prefilter (every position reads its bucket)
+#define L7M_ALIT_BLOOM_BITS 0  // log2 of the prefilter's bits; 0: no prefilter (every position reads its bucket)
 #endif
 constexpr uint32_t kAlitBloomBits = L7M_ALIT_BLOOM_BITS;
 constexpr uint32_t kAlitBloomWords = kAlitBloomBits ? (1u << kAlitBloomBits) / 32u : 0u;

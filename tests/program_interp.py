@@ -41,6 +41,7 @@ DFA_WORDS = 32  # sizeof(DfaDesc) / 4
 DFA_SEARCH = 1  # program.h kDfaSearch
 DFA_ALIT = 2    # program.h kDfaAlit
 DCAP_SHIFT, PAT_MASK = 24, (1 << 24) - 1  # program.h kDcapShift / kPatMask
+ALIT_BLOOM_BITS = 0  # program.h L7M_ALIT_BLOOM_BITS of the default build (prefilter off)
 
 
 def gram_bucket(g):
@@ -122,10 +123,13 @@ class HttpProgram:
             for eg, ep in ((e[0], e[1]), (e[2], e[3])):
                 if not ep or eg != g:
                     continue
-                # the kernel probes the bucket only where the prefilter bit
-                # (program.h kAlitBloomWords) is set: no table gram may lack it
-                bb = (gram_bucket(g) >> 8) & 0x3FFF
-                assert (self.img[tab - 512 + (bb >> 5)] >> (bb & 31)) & 1, "alit prefilter misses a table gram"
+                # a build with the prefilter (program.h L7M_ALIT_BLOOM_BITS)
+                # probes the bucket only where the gram's bit is set: no
+                # table gram may lack it
+                if ALIT_BLOOM_BITS:
+                    bb = (gram_bucket(g) >> 8) & ((1 << ALIT_BLOOM_BITS) - 1)
+                    assert (self.img[tab - (1 << ALIT_BLOOM_BITS) // 32 + (bb >> 5)] >> (bb & 31)) & 1, \
+                        "alit prefilter misses a table gram"
                 words, byts = (self.img, self.img_bytes) if fd[13] else (self.w, self.prog_bytes)  # alit_lds
                 r = pats + 4 * (ep - 1)  # AlitRec: header granule, then L's bytes
                 len_k, code, resid, _ = words[r:r + 4]

@@ -5,18 +5,20 @@
 # lines, rocprofv3 kernel-trace summaries of the same runs, FETCH_SIZE /
 # WRITE_SIZE passes (tools/traffic.py) for configs 2, 3 and 5.
 #   tools/gpu_r6_evidence.sh TAG [part]   -> gpurun_out/TAG/...
-# part: all (default) | bench | trace | pmc
+# part: all (default) | bench1 | bench2 | trace | pmc (one gpurun call each)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r6e}; PART=${2:-all}
 OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 step() { local name=$1 secs=$2; shift 2; echo "== $name: $*" >> $OUT/steps.log
   timeout -k 10 $secs "$@" > $OUT/$name.out 2> $OUT/$name.err; local rc=$?; echo "$name rc=$rc" | tee -a $OUT/steps.log; return $rc; }
-if [ "$PART" = all ] || [ "$PART" = bench ]; then
+if [ "$PART" = all ] || [ "$PART" = bench1 ]; then
   step gpu_suite 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit $?
   step bench_cfg2 700 python3 -u bench.py || exit $?
   step bench_cfg1 400 python3 -u bench.py --config 1 || exit $?
   step bench_cfg3 600 python3 -u bench.py --config 3 || exit $?
+fi
+if [ "$PART" = all ] || [ "$PART" = bench2 ]; then
   step bench_cfg5 600 python3 -u bench.py --config 5 --no-e2e || exit $?
   step bench_re2 400 python3 -u bench.py --dialect re2 --no-batcher --no-e2e || exit $?
   step bench_ext 400 python3 -u bench.py --extended --no-batcher --no-e2e || exit $?
