@@ -137,6 +137,23 @@ def test_forced_capture_backreferences_first_pass_match_oracle():
     assert len(prog.dcaps) == 1 and prog.h["n_slow"] == 1
 
 
+def test_forced_capture_analysis_differential_fuzz():
+    """tests/cpp/fuzz_dcap.cc: random P1 (C{n,m}) L2 \\1 R patterns and near
+    misses; wherever regex_ecma.h analyze_dcap accepts one, the first-pass
+    decision (P1, maximal class run, L2, the run repeated, R's automaton)
+    equals std::regex_match on every subject."""
+    exe = "/tmp/l7m_fuzz_dcap"
+    src = os.path.join(ROOT, "tests", "cpp", "fuzz_dcap.cc")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-o", exe, src,
+                           os.path.join(ROOT, "cilium_amd", "csrc", "regex_ecma.cc"),
+                           os.path.join(ROOT, "cilium_amd", "csrc", "dfa_pack.cc"),
+                           os.path.join(ROOT, "cilium_amd", "csrc", "regex_vm.cc")])
+    for seed in ("5", "6"):
+        out = subprocess.run(["timeout", "240", exe, seed, "2000", "200"], capture_output=True, text=True)
+        assert out.returncode == 0, out.stdout[-3000:]
+        assert "mismatches=0" in out.stdout
+
+
 def test_unknown_dialect_is_rejected():
     with pytest.raises(L.L7Error) as e:
         L.RuleSet.compile_http([L.PortRuleHTTP(Path="/a")], dialect=7)
