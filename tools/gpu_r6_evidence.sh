@@ -24,6 +24,9 @@ if [ "$PART" = all ] || [ "$PART" = bench2 ]; then
   step bench_ext 400 python3 -u bench.py --extended --no-batcher --no-e2e || exit $?
   step bench_cfg4 900 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 \
     --master-port 29517 bench.py --config 4 --gpus 2 --backend gloo --no-cpu-baseline --no-e2e --no-batcher || exit $?
+  for f in 3 4 5 6; do  # batcher flushers (in_flight) at 8 eager callers, config 2
+    L7M_IN_FLIGHT=$f step batcher_if$f 120 cilium_amd/batcher_bench 2 1000000 3 1 8 || exit $?
+  done
 fi
 if [ "$PART" = all ] || [ "$PART" = trace ]; then
   for v in cfg2 cfg1 cfg3 cfg5 re2 ext; do
