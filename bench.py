@@ -262,6 +262,15 @@ def measured_traffic(cfg):
     return None
 
 
+def emit(res):
+    """Print the bench line, naming the device code it measured (the md5 of
+    the library's gfx950 code objects, cilium_amd/codehash.py: the key that
+    ties rocprof summaries and traffic files under profiles/ to a build)."""
+    from cilium_amd.codehash import kernel_md5
+    res["kernel_md5"] = kernel_md5(L.LIB_PATH)
+    print(json.dumps(res), flush=True)
+
+
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -434,7 +443,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(cfg, rules, args.cpu_baseline_seconds,
                                                args.threads or host_cores()["usable"], dialect=dialect,
                                                n_rules=c["n_rules"])
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         dist.destroy_process_group()
 
@@ -503,7 +512,7 @@ def run_single_process(args, scaling):
     }
     if not args.no_parity:
         res["parity"] = parity_leg(cfg, rules, got, 0, n_job, threads, n_sample=args.parity_sample)
-    print(json.dumps(res), flush=True)
+    emit(res)
     ds.close()
 
 
@@ -650,7 +659,7 @@ def run_mixed(args, world, rank, dev, scaling):
                                "sample": "; ".join(samples) + f" (oracle/l7oracle.cc on {threads} threads); "
                                          f"single_thread_value: {n1} requests of part config {p['gcfg']} on 1 "
                                          f"thread"}
-    print(json.dumps(res), flush=True)
+    emit(res)
     if world > 1:
         dist.destroy_process_group()
 
