@@ -246,28 +246,30 @@ def cpu_model():
 def measured_traffic(cfg):
     """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE
     passes (tools/traffic.py) of THIS kernel build (matched by the .so hash,
-    or by the hash of its device code objects, cilium_amd/codehash.py) on the
+    or by the hashes of its device code, cilium_amd/codehash.py) on the
     default workload; None when no such measurement exists."""
     import glob
     import hashlib
-    from cilium_amd.codehash import kernel_md5
+    from cilium_amd.codehash import code_md5, kernel_md5
     with open(L.LIB_PATH, "rb") as f:
         md5 = hashlib.md5(f.read()).hexdigest()
     kmd5 = kernel_md5(L.LIB_PATH)
+    cmd5 = code_md5(L.LIB_PATH)
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"traffic_cfg{cfg}.json")), reverse=True):
         with open(path) as f:
             t = json.load(f)
-        if t.get("so_md5") == md5 or t.get("kernel_md5") == kmd5:
+        if t.get("so_md5") == md5 or t.get("kernel_md5") == kmd5 or t.get("code_md5") == cmd5:
             return float(t["traffic_bytes"])
     return None
 
 
 def emit(res):
-    """Print the bench line, naming the device code it measured (the md5 of
-    the library's gfx950 code objects, cilium_amd/codehash.py: the key that
-    ties rocprof summaries and traffic files under profiles/ to a build)."""
-    from cilium_amd.codehash import kernel_md5
-    res["kernel_md5"] = kernel_md5(L.LIB_PATH)
+    """Print the bench line, naming the device code it measured
+    (cilium_amd/codehash.py code_md5: the md5 of the library's gfx950 code,
+    stable across rebuilds of the same source -- the key that ties rocprof
+    summaries and traffic files under profiles/ to a build)."""
+    from cilium_amd.codehash import code_md5
+    res["code_md5"] = code_md5(L.LIB_PATH)
     print(json.dumps(res), flush=True)
 
 

@@ -1419,7 +1419,15 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
   // (small batches: the offsets may sit in pinned host memory, across PCIe).
   const uint64_t gw = wave_index;
   const uint64_t nw = wave_count;
+#if L7M_SPEC_TILE
+  // (kSpecTile) a small batcher batch: wave 0 takes it whole
+  const bool spec = done.flag && n <= 64 && arena_bytes <= stage;
+  const uint64_t start = spec ? 0 : n * gw / nw;
+  const uint64_t end = spec ? (gw == 0 ? n : 0) : n * (gw + 1) / nw;
+#else
   const uint64_t end = n * (gw + 1) / nw;
+#define start (n * gw / nw)
+#endif
   auto load_offs = [&](uint64_t cur, uint64_t* o, uint64_t* onext) {
     *o = 0;
     *onext = 0;
@@ -1429,7 +1437,23 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
     }
   };
   uint64_t o1, n1, o2, n2;
-  load_offs(n * gw / nw, &o1, &n1);
+  load_offs(start, &o1, &n1);
+#if L7M_SPEC_TILE
+  if (spec && gw == 0) {
+    // the batch's bytes from offset 0, before the offsets (pinned host
+    // memory: both requests cross PCIe; plan() below checks the guess)
+    const u32x4* src = reinterpret_cast<const u32x4*>(arena);
+#pragma unroll
+    for (uint32_t it = 0; it < kCopyIters; ++it) {
+      const uint32_t q = it * 64u + lane;
+      if (q * 16u < arena_bytes)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + q),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(stg + it * 1024u)),
+                                         16, 0, 2);
+    }
+  }
+#endif
   if (load_image) {
     const uint4* g = reinterpret_cast<const uint4*>(prog + h.lds_image_off);
     uint4* l = reinterpret_cast<uint4*>(img);
@@ -1532,8 +1556,16 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
           __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(arena + o + 128ull * j), junk, 4, 0, 0);
     }
   };
-  Tile t = plan(n * gw / nw, o1, n1);
+  Tile t = plan(start, o1, n1);
+#if L7M_SPEC_TILE
+  if (!(spec && t.base == 0 && t.take == t.k)) {  // (a tile at offset 0 is what the guess requested)
+    if (spec) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the guessed bytes have landed first
+    issue_bytes(t);
+  }
+#else
+#undef start
   issue_bytes(t);
+#endif
   load_offs(t.cur + t.take, &o2, &n2);
   while (t.cur < end) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's LDS-DMA pieces have landed

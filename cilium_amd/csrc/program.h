@@ -158,6 +158,14 @@ constexpr uint32_t kMaxLdsCounters = 8192;       // per-rule hit counters kept i
 // workgroup (workgroup-scope atomics in L2) instead of LDS, so the record
 // stage gets their LDS
 constexpr bool kSliceHits = L7M_SLICE_HITS != 0;
+#ifndef L7M_SPEC_TILE
+#define L7M_SPEC_TILE 0
+#endif
+// (experiment) batcher launches (a DoneSignal, <= 64 records, the whole batch
+// within one record stage): the first wave takes every record and requests
+// the batch's bytes from offset 0 before the offsets have arrived, so the
+// two PCIe round trips to the pinned batch overlap
+constexpr bool kSpecTile = L7M_SPEC_TILE != 0;
 constexpr uint32_t kHttpMinStage = 2048;         // smallest record stage per wave (bytes)
 #ifndef L7M_HTTP_MAX_STAGE
 #define L7M_HTTP_MAX_STAGE 8192

@@ -44,3 +44,12 @@ def test_kernel_code_hash_covers_both_kernel_objects():
     assert n_gfx == 6
     k = kernel_md5(L.LIB_PATH)
     assert k == kernel_md5(L.LIB_PATH) and k != hashlib.md5(data).hexdigest()
+    # the code hash reads the ELF sections of every code object (6 of them)
+    from cilium_amd.codehash import _code_objects, _elf_sections, code_md5
+    objs = list(_code_objects(data))
+    assert len(objs) == 6
+    for _, obj in objs:
+        names = {nm for nm, _ in _elf_sections(obj)}
+        assert {b".text", b".rodata", b".note"} <= names
+    c = code_md5(L.LIB_PATH)
+    assert c == code_md5(L.LIB_PATH) and c != k

@@ -39,10 +39,11 @@ def main():
     kib_f = max(fetch)  # the timed launch (largest dispatch)
     kib_w = max(write)
     sys.path.insert(0, ROOT)
-    from cilium_amd.codehash import kernel_md5
+    from cilium_amd.codehash import code_md5, kernel_md5
     res = {"config": int(cfg), "fetch_kib": kib_f, "write_kib": kib_w,
            "traffic_bytes": (2 * kib_f + kib_w) * 1024, "so_md5": so_hash(),
            "kernel_md5": kernel_md5(os.path.join(ROOT, "cilium_amd", "libl7match.so")),
+           "code_md5": code_md5(os.path.join(ROOT, "cilium_amd", "libl7match.so")),
            "correction": "2 x FETCH_SIZE (gfx950 half-count on wide streams) + WRITE_SIZE, KiB -> bytes"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
