@@ -1668,6 +1668,16 @@ __device__ __forceinline__ void http_eval_body(const uint32_t* __restrict__ prog
       if (x) atomicAdd(hits + i, static_cast<unsigned long long>(x));
     }
   }
+#if L7M_SPEC_TILE
+  if (spec && kHits == kNoHits) {
+    // wave 0 decided the whole batch: it alone signals (no counter round trip)
+    if (gw == 0) {
+      __threadfence_system();
+      if (lane == 0) __hip_atomic_store(done.flag, done.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
+#endif
   if (done.flag) {  // (l7m_device.h DoneSignal)
     __threadfence_system();  // this wave's verdict stores (and counters) are visible system-wide
     if (lane == 0 && atomicAdd(done.ctr, 1u) == wave_count - 1u) {
