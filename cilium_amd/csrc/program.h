@@ -159,12 +159,15 @@ constexpr uint32_t kMaxLdsCounters = 8192;       // per-rule hit counters kept i
 // stage gets their LDS
 constexpr bool kSliceHits = L7M_SLICE_HITS != 0;
 #ifndef L7M_SPEC_TILE
-#define L7M_SPEC_TILE 0
+#define L7M_SPEC_TILE 1
 #endif
-// (experiment) batcher launches (a DoneSignal, <= 64 records, the whole batch
-// within one record stage): the first wave takes every record and requests
-// the batch's bytes from offset 0 before the offsets have arrived, so the
-// two PCIe round trips to the pinned batch overlap
+// Batcher launches (a DoneSignal, <= 64 records, the whole batch within one
+// record stage): the first wave takes every record and requests the batch's
+// bytes from offset 0 before the offsets have arrived, so the two PCIe round
+// trips to the pinned batch overlap, and it alone signals completion (no
+// per-wave counter).  Measured (profiles/r06/ab_spec_tile_r6g.jsonl, config
+// 2, 8 callers, alternated on one box): gpu phase 17.5 -> 16.1 us, 270 ->
+// 293 k/s; the 64 M-request launch 4.095 -> 4.065 ms.  0: the round-5 path.
 constexpr bool kSpecTile = L7M_SPEC_TILE != 0;
 constexpr uint32_t kHttpMinStage = 2048;         // smallest record stage per wave (bytes)
 #ifndef L7M_HTTP_MAX_STAGE
