@@ -5,7 +5,8 @@
 # lines, rocprofv3 kernel-trace summaries of the same runs, FETCH_SIZE /
 # WRITE_SIZE passes (tools/traffic.py) for configs 2, 3 and 5.
 #   tools/gpu_r6_evidence.sh TAG [part]   -> gpurun_out/TAG/...
-# part: all (default) | bench1 | bench2 | bench3 | trace | pmc (one gpurun call each)
+# part: all (default) | pmc | bench1 | bench2 | trace (one gpurun call each; pmc first, so
+# that the bench lines find the traffic of their own device code)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r6e}; PART=${2:-all}
@@ -24,16 +25,8 @@ if [ "$PART" = all ] || [ "$PART" = bench2 ]; then
   step bench_ext 400 python3 -u bench.py --extended --no-batcher --no-e2e || exit $?
   step bench_cfg4 900 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 \
     --master-port 29517 bench.py --config 4 --gpus 2 --backend gloo --no-cpu-baseline --no-e2e --no-batcher || exit $?
-  for f in 3 4 5 6; do  # batcher flushers (in_flight) at 8 eager callers, config 2
-    L7M_IN_FLIGHT=$f step batcher_if$f 120 cilium_amd/batcher_bench 2 1000000 3 1 8 || exit $?
-  done
-fi
-if [ "$PART" = all ] || [ "$PART" = bench3 ]; then
   step bench_cfg4_n1 600 python3 -u bench.py --config 4 --no-e2e || exit $?
-  # the batcher alone (default flushers) and then bench.py's batcher leg and
-  # cpu_baseline on the same box
   step batcher_solo 120 cilium_amd/batcher_bench 2 1000000 3 1 8 || exit $?
-  step bench_cfg2_b 700 python3 -u bench.py --no-e2e || exit $?
 fi
 if [ "$PART" = all ] || [ "$PART" = trace ]; then
   for v in cfg2 cfg1 cfg3 cfg5 re2 ext; do
