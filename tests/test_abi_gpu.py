@@ -185,3 +185,46 @@ def test_batcher_idle_gap_and_rule_switches(gpu):
     assert p["requests"] == 3 * len(recs_a) + 2 * len(recs_b) + len(recs_c)
     assert 1 <= p["batches"] <= p["requests"] and p["fill_us"] >= 0.0
     b.close()
+
+
+def test_batcher_small_batches_both_staging_paths(gpu):
+    """program.h L7M_SPEC_TILE: a batcher launch of <= 64 records whose bytes
+    fit one record stage is taken whole by the first wave, which requests the
+    batch's bytes before its offsets and alone signals completion; larger
+    batches (more records, or more bytes than a stage) take the per-wave
+    path, and a record longer than the stage is read from memory by its lane.
+    Batches of 1 / 40 / 64 / 65 concurrent callers over records of ~80 B,
+    ~200 B (40 fit a stage, 64 do not) and ~9 KB: every verdict equals the
+    oracle's."""
+    import threading
+    rng = np.random.default_rng(11)
+    rules = [L.PortRuleHTTP(Path="/a/[a-z]+", Method="GET", Headers=["X-Pad"]),
+             L.PortRuleHTTP(Path="/b/[0-9]+", Method="POST"),
+             L.PortRuleHTTP(Path="/c/.*", Host="h[0-9]\\.example")]
+    rs = L.RuleSet.compile_http(rules)
+    for pad in (0, 120, 9000):
+        reqs = []
+        for i in range(65):
+            hdr = [("x-pad", "p" * (pad + int(rng.integers(0, 8))))] if pad or rng.random() < 0.5 else []
+            reqs.append(L.HTTPRequest(str(rng.choice(["GET", "POST"])),
+                                      str(rng.choice(["/a/xyz", "/b/123", "/c/q", "/b/x", "/d"])),
+                                      str(rng.choice(["h1.example", "hx.example"])), hdr))
+        ar, of = L.pack_http(reqs)
+        recs = [ar[int(of[i]):int(of[i + 1]) if i + 1 < len(of) else ar.nbytes].tobytes() for i in range(len(of))]
+        exp = HttpOracle(rules).eval(ar, of)
+        for k in (1, 40, 64, 65):
+            b = L.Batcher(rs, max_batch=64, max_delay_us=200_000, in_flight=2)
+            got = np.full(k, -100, dtype=np.int64)
+            go = threading.Barrier(k)
+
+            def worker(i):
+                go.wait()
+                got[i] = b.eval(recs[i])
+
+            th = [threading.Thread(target=worker, args=(i,)) for i in range(k)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            b.close()
+            assert np.array_equal(got, exp[:k]), (pad, k)
