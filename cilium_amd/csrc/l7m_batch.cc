@@ -379,32 +379,104 @@ struct l7m_batcher {
     idle_cv.notify_one();
   }
 
+  // Per-batch bookkeeping once its verdicts are in (or its launch failed).
+  void finish(Batch* b, l7m_ruleset* r, uint32_t cnt, int rc, int64_t t_close, int64_t t_launch) {
+    const int64_t t_done = now_ns();
+    l7m_release(r);
+    batches.fetch_add(1);
+    requests.fetch_add(cnt);
+    const int64_t t_first = b->first_ns.load();
+    if (t_first > 0 && t_close > t_first) {  // a batch without its stamp is left out of the fill phase
+      fill_ns.fetch_add(static_cast<uint64_t>(t_close - t_first));
+      fill_batches.fetch_add(1);
+    }
+    launch_ns.fetch_add(static_cast<uint64_t>(t_launch - t_close));
+    gpu_ns.fetch_add(static_cast<uint64_t>(t_done - t_launch));
+    b->rc = rc;
+    b->done_ns = t_done;
+    b->readers.store(cnt);
+    b->done.store(1);  // seq_cst with the callers' sleepers increment (no lost wake-up)
+    if (b->sleepers.load()) {
+      std::lock_guard<std::mutex> g(b->m);
+      b->cv.notify_all();
+    }
+  }
+
+  // A flusher keeps up to `pipe` kernel-signalled HTTP launches in flight,
+  // one per slot (own stream, own completion word), and goes back to the
+  // fill while they run; pipe 1 waits for each launch before the next batch.
+  struct Slot {
+    hipStream_t stream = nullptr;
+    uint32_t* ctr = nullptr;   // device: the kernel's wave counter
+    uint32_t* host = nullptr;  // pinned: the completion word
+    void* dev = nullptr;       // its device address
+    uint32_t seq = 0;
+    bool busy = false;
+    Batch* b = nullptr;
+    l7m_ruleset* r = nullptr;
+    uint32_t cnt = 0, spins = 0;
+    int64_t t_close = 0, t_launch = 0;
+  };
+  uint32_t pipe = 1;
+
   void run() {
     (void)hipSetDevice(device);
-    hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;
-    const bool dev_ok = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess &&
-                        hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    std::vector<Slot> slots(pipe);
+    bool dev_ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
     // HTTP launches signal their completion by a pinned host word the kernel
     // stores last (l7m_device.h DoneSignal): polled in place of an event,
     // whose completion the host sees only after the command processor's
     // end-of-kernel signal
-    uint32_t* sig_ctr = nullptr;
-    uint32_t* sig_host = nullptr;
-    void* sig_dev = nullptr;
-    uint32_t sig_seq = 0;
-    bool sig_ok = dev_ok && hipMalloc(reinterpret_cast<void**>(&sig_ctr), 64) == hipSuccess &&
-                  hipMemset(sig_ctr, 0, 64) == hipSuccess &&
-                  hipHostMalloc(reinterpret_cast<void**>(&sig_host), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
-                      hipSuccess &&
-                  hipHostGetDevicePointer(&sig_dev, sig_host, 0) == hipSuccess && sig_dev;
-    if (sig_host) std::memset(sig_host, 0, 64);
+    bool sig_ok = dev_ok;
+    for (Slot& q : slots) {
+      dev_ok = dev_ok && hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) == hipSuccess;
+      sig_ok = sig_ok && dev_ok && hipMalloc(reinterpret_cast<void**>(&q.ctr), 64) == hipSuccess &&
+               hipMemset(q.ctr, 0, 64) == hipSuccess &&
+               hipHostMalloc(reinterpret_cast<void**>(&q.host), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
+                   hipSuccess &&
+               hipHostGetDevicePointer(&q.dev, q.host, 0) == hipSuccess && q.dev;
+      if (q.host) std::memset(q.host, 0, 64);
+    }
+    sig_ok = sig_ok && dev_ok;
     if (std::getenv("L7M_NO_SIGNAL")) sig_ok = false;
+    hipStream_t stream = slots[0].stream;  // unsignalled launches (after the slots have drained)
+    uint32_t npending = 0;
+    // Completes the in-flight launches whose word has arrived (all of them
+    // when `all`); the stream is checked now and then so that a failed launch
+    // cannot leave a slot pending.
+    auto poll = [&](bool all) {
+      for (;;) {
+        for (Slot& q : slots) {
+          if (!q.busy) continue;
+          int rc = L7M_OK;
+          bool done = __atomic_load_n(q.host, __ATOMIC_ACQUIRE) == q.seq;
+          if (!done && (++q.spins & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(q.stream);
+            if (e != hipErrorNotReady) {
+              done = true;
+              if (e != hipSuccess || __atomic_load_n(q.host, __ATOMIC_ACQUIRE) != q.seq) rc = L7M_EDEVICE;
+            }
+          }
+          if (!done) continue;
+          q.busy = false;
+          --npending;
+          finish(q.b, q.r, q.cnt, rc, q.t_close, q.t_launch);
+        }
+        if (!all || npending == 0) return;
+        cpu_relax();
+      }
+    };
     for (;;) {
+      if (npending) poll(false);
       Batch* b = cur.load(std::memory_order_acquire);
       const uint64_t s0 = b->resv.load(std::memory_order_acquire);
       const uint32_t cnt0 = count_of(s0);
       if (cnt0 == 0) {
+        if (npending) {  // launches in flight: keep polling them
+          cpu_relax();
+          continue;
+        }
         if (stop.load()) break;
         // idle: poll a little, then sleep until a caller's first append
         const int64_t t0 = now_ns();
@@ -437,6 +509,10 @@ struct l7m_batcher {
       const int64_t free_callers = static_cast<int64_t>(callers.load()) - closed_now;
       if (!eager && !stop.load() && cnt0 < max_batch && !b->want_close.load() && static_cast<int64_t>(cnt0) < free_callers &&
           (first == 0 || now_ns() - first < static_cast<int64_t>(max_delay_us) * 1000)) {
+        cpu_relax();
+        continue;
+      }
+      if (npending == pipe) {  // every slot in flight: this batch waits for one
         cpu_relax();
         continue;
       }
@@ -473,7 +549,7 @@ struct l7m_batcher {
       int kind = 0;
       uint32_t stage = 0;
       uint64_t serial = 0;
-      int64_t t_launch;
+      int64_t t_launch = t_close;
       bool normal = true;
       if (rc == L7M_OK && res.ok && cnt <= kResidentMax &&
           l7m::resident_program(r, &dprog, &kind, &stage, &serial)) {
@@ -485,62 +561,57 @@ struct l7m_batcher {
       if (normal) {
         bool signalled = false;
         if (rc == L7M_OK && info.proto == L7M_PROTO_HTTP && sig_ok) {
-          const l7m::DoneSignal sg{sig_ctr, static_cast<uint32_t*>(sig_dev), ++sig_seq ? sig_seq : ++sig_seq};
-          rc = l7m::eval_device_signal(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, stream, sg, &signalled);
+          Slot* q = nullptr;
+          for (Slot& x : slots)
+            if (!x.busy) {
+              q = &x;
+              break;
+            }
+          // (npending < pipe above: a slot is free)
+          if (!++q->seq) ++q->seq;
+          const l7m::DoneSignal sg{q->ctr, static_cast<uint32_t*>(q->dev), q->seq};
+          rc = l7m::eval_device_signal(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, q->stream, sg, &signalled);
+          t_launch = now_ns();
+          if (rc == L7M_OK && signalled) {
+            // the kernel's deciding wave stores q->seq after every verdict is
+            // visible (l7m_device.h DoneSignal); poll() completes the batch
+            q->busy = true;
+            q->b = b;
+            q->r = r;
+            q->cnt = cnt;
+            q->spins = 0;
+            q->t_close = t_close;
+            q->t_launch = t_launch;
+            ++npending;
+            if (npending == pipe) poll(false);
+            continue;
+          }
+          stream = q->stream;
         } else if (rc == L7M_OK) {
+          poll(true);  // unsignalled launches wait for an event: no slot in flight meanwhile
+          stream = slots[0].stream;
           rc = info.proto == L7M_PROTO_KAFKA
                    ? l7m_eval_device_ids(r, b->d_arena, bytes, b->d_offs, cnt, b->d_ids, b->d_verd, nullptr, stream, 0)
                    : l7m_eval_device(r, b->d_arena, bytes, b->d_offs, cnt, b->d_verd, nullptr, stream, 0);
+          t_launch = now_ns();
         }
-        t_launch = now_ns();
-        if (rc == L7M_OK && signalled) {
-          // the kernel's last wave stores sig_seq after every verdict is
-          // visible; the stream is checked now and then so that a failed
-          // launch cannot leave the flusher spinning
-          for (uint32_t spin = 1;; ++spin) {
-            if (__atomic_load_n(sig_host, __ATOMIC_ACQUIRE) == sig_seq) break;
-            if ((spin & 1023) == 0) {
-              const hipError_t q = hipStreamQuery(stream);
-              if (q == hipErrorNotReady) continue;
-              if (q != hipSuccess || __atomic_load_n(sig_host, __ATOMIC_ACQUIRE) != sig_seq) rc = L7M_EDEVICE;
-              break;
-            }
-            cpu_relax();
-          }
-        } else {
-          if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
-          if (rc == L7M_OK) {
-            hipError_t q;
-            while ((q = hipEventQuery(ev)) == hipErrorNotReady) cpu_relax();
-            if (q != hipSuccess) rc = L7M_EDEVICE;
-          }
+        if (rc == L7M_OK && hipEventRecord(ev, stream) != hipSuccess) rc = L7M_EDEVICE;
+        if (rc == L7M_OK) {
+          hipError_t e;
+          while ((e = hipEventQuery(ev)) == hipErrorNotReady) cpu_relax();
+          if (e != hipSuccess) rc = L7M_EDEVICE;
         }
       }
-      const int64_t t_done = now_ns();
-      l7m_release(r);
-      batches.fetch_add(1);
-      requests.fetch_add(cnt);
-      const int64_t t_first = b->first_ns.load();
-      if (t_first > 0 && t_close > t_first) {  // a batch without its stamp is left out of the fill phase
-        fill_ns.fetch_add(static_cast<uint64_t>(t_close - t_first));
-        fill_batches.fetch_add(1);
-      }
-      launch_ns.fetch_add(static_cast<uint64_t>(t_launch - t_close));
-      gpu_ns.fetch_add(static_cast<uint64_t>(t_done - t_launch));
-      b->rc = rc;
-      b->done_ns = t_done;
-      b->readers.store(cnt);
-      b->done.store(1);  // seq_cst with the callers' sleepers increment (no lost wake-up)
-      if (b->sleepers.load()) {
-        std::lock_guard<std::mutex> g(b->m);
-        b->cv.notify_all();
-      }
+      finish(b, r, cnt, rc, t_close, t_launch);
     }
-    if (stream) (void)hipStreamSynchronize(stream);
-    if (sig_ctr) (void)hipFree(sig_ctr);
-    if (sig_host) (void)hipHostFree(sig_host);
+    poll(true);
+    for (Slot& q : slots) {
+      if (q.stream) (void)hipStreamSynchronize(q.stream);
+      if (q.ctr) (void)hipFree(q.ctr);
+      if (q.host) (void)hipHostFree(q.host);
+      if (q.stream) (void)hipStreamDestroy(q.stream);
+    }
     if (ev) (void)hipEventDestroy(ev);
-    if (stream) (void)hipStreamDestroy(stream);
   }
 
   // A record that can never fit a batch: evaluated alone (copying path).
@@ -660,6 +731,10 @@ int l7m_batcher_create(l7m_ruleset* rs, const l7m_batcher_opts* opts, l7m_batche
   l7m_retain(rs);
   b->rs = rs;
   b->resident_init();
+  if (const char* e = std::getenv("L7M_PIPE")) {  // (experiment) launches in flight per flusher
+    const int v = std::atoi(e);
+    b->pipe = v < 1 ? 1u : v > 4 ? 4u : static_cast<uint32_t>(v);
+  }
   for (uint32_t i = 0; i < b->in_flight; ++i) b->flushers.emplace_back([b] { b->run(); });
   *out = b;
   return L7M_OK;
